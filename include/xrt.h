@@ -1,0 +1,207 @@
+/*
+ * xrt.h — C ABI of libxrt_hip.so, the MI355X (gfx950) path-tracing backend that sits
+ * behind the reference's Renderer::render() (Src/renderer.h:15).
+ *
+ * The reference has no FFI: its plugin surface is the C++ virtual class
+ *   virtual void Renderer::render(const Scene&, Sampler::SamplerType, Image&) const = 0;
+ * (Src/renderer.h:8-20).  A renderer that replaces NormalRenderer / ParallelRenderer
+ * (Src/renderer.cpp:8-27, 83-99) needs exactly four things from the caller's objects:
+ *   - the scene's objects in Scene::m_objects iteration order (Src/scene.h:45, scene.cpp:190-211),
+ *   - the area lights in Scene::m_areaLights order             (Src/scene.h:44, scene.cpp:166-188),
+ *   - the pinhole camera (c2w, scale, aspect)                   (Src/camera.h:10-11,37-60),
+ *   - the integrator kind and its max depth                     (Src/integrator.h:198-291,76-120,401-478),
+ * and it must fill an Image of W*H float3 in place with the per-pixel sample mean
+ * (Src/renderer.cpp:29-81,98; Src/image.h:46-78).  Every entry point below maps onto
+ * one of those steps.  The C++ HipRenderer (include/xrt/renderer.h) is the
+ * reference-side binding; INTEGRATION.md shows it.
+ *
+ * Conventions: plain C types only; the caller owns all host memory and the library
+ * copies what it needs; status 0 = XRT_OK, negative = error (xrt_last_error gives
+ * text); no C++ exception crosses this boundary.  One context = one GPU = one host
+ * thread; multi-GPU runs one process (and one context) per GPU.
+ */
+#ifndef XRT_H
+#define XRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XRT_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------- */
+enum {
+    XRT_OK = 0,
+    XRT_ERR_INVALID = -1,     /* bad argument / inconsistent scene */
+    XRT_ERR_HIP = -2,         /* HIP runtime error (no GPU, launch failure, fault) */
+    XRT_ERR_STATE = -3,       /* call order: e.g. render before upload */
+    XRT_ERR_OOM = -4,         /* device allocation failed */
+    XRT_ERR_UNSUPPORTED = -5, /* feature outside the supported set */
+    XRT_ERR_IO = -6           /* file could not be read / parsed (Scene::loadObj exit(1)) */
+};
+
+/* ---- scene description (flattened Scene) ------------------------------------------ */
+enum { XRT_OBJ_MESH = 0, XRT_OBJ_SPHERE = 1, XRT_OBJ_BOX = 2 };
+enum { XRT_LIGHT_QUAD = 0, XRT_LIGHT_TRIANGLE = 1, XRT_LIGHT_SPHERE = 2 };
+enum { XRT_MAT_NONE = 0, XRT_MAT_LAMBERT = 1 };
+
+/* One Object (Src/primitive.h:40-95) in Scene::m_objects iteration order. */
+typedef struct {
+    int32_t kind;       /* XRT_OBJ_*                                                     */
+    int32_t first;      /* first primitive in the kind's array (tris / spheres / boxes)  */
+    int32_t count;      /* number of primitives (mesh: triangles; sphere/box: 1)         */
+    int32_t material;   /* XRT_MAT_* (Object::m_material != nullptr)                     */
+    float albedo[3];    /* Lambert::m_albedo (Src/material.h:76)                         */
+    int32_t light;      /* index into lights[] or -1 (Object::m_areaLight)               */
+    int32_t medium;     /* 0 = the scene medium, -1 = none (Object::m_medium)            */
+} xrt_object;
+
+/* One AreaLight (Src/light.h:54-210) in Scene::m_areaLights order, world space. */
+typedef struct {
+    int32_t kind;       /* XRT_LIGHT_*                                                   */
+    float v0[3];        /* quad / triangle vertices after multVecMatrix(l2w)             */
+    float v1[3];
+    float v2[3];
+    float center[3];    /* sphere light                                                  */
+    float radius;
+    float Le[3];        /* AreaLight::Le_                                                */
+} xrt_light;
+
+typedef struct {
+    uint32_t n_objects;
+    const xrt_object* objects;
+    uint32_t n_tris;
+    const float* tri_v;      /* [n_tris][3][3] vertices (Primitive::m_vertices)       */
+    const float* tri_n;      /* [n_tris][3][3] vertex normals (Primitive::m_normals)  */
+    uint32_t n_spheres;
+    const float* spheres;    /* [n_spheres][4] center.xyz, radius                      */
+    uint32_t n_boxes;
+    const float* boxes;      /* [n_boxes][6] pMin.xyz, pMax.xyz (AABB)                 */
+    uint32_t n_lights;
+    const xrt_light* lights;
+} xrt_scene_desc;
+
+/* Dense density grid standing in for DensityGrid (Src/grid.h:9-15): OpenVDB
+ * BoxSampler::wsSample semantics — world -> index by (p - origin) / voxel_size, voxel
+ * centres at integer index coordinates, trilinear, background 0 outside the data. */
+typedef struct {
+    uint32_t nx, ny, nz;
+    const float* density;    /* [nz][ny][nx]                                           */
+    float origin[3];         /* world position of index (0,0,0)                         */
+    float voxel_size;
+    float bbox_min[3];       /* DensityGrid::getBounds() (world)                        */
+    float bbox_max[3];
+    float max_density;       /* DensityGrid::getMaxDensity()                            */
+    float g;                 /* HenyeyGreenstein g                                      */
+    float absorption[3];     /* HeterogeneousMedium::absorptionColor                    */
+    float scattering[3];     /* HeterogeneousMedium::scatteringColor                    */
+    float density_multiplier;
+} xrt_medium_desc;
+
+/* ---- render parameters --------------------------------------------------------------- */
+enum { XRT_INTEGRATOR_GI = 0, XRT_INTEGRATOR_DIRECT = 1, XRT_INTEGRATOR_VPT = 2 };
+enum { XRT_FLAG_TIMING = 1u };   /* time every kernel with HIP events (xrt_stats.kernel_ms) */
+
+typedef struct {
+    int32_t integrator;      /* XRT_INTEGRATOR_*                                        */
+    uint32_t max_depth;      /* GIIntegrator / VolumePathTracing m_maxDepth             */
+    uint32_t width, height;  /* Image size                                              */
+    uint32_t spp;            /* NormalRenderer::n_samples                               */
+    uint32_t shard_index;    /* this rank owns image rows y with y % shard_count == idx */
+    uint32_t shard_count;    /* 1 = whole image                                         */
+    uint32_t flags;          /* XRT_FLAG_*                                              */
+} xrt_render_params;
+
+enum { XRT_K_SEED = 0, XRT_K_TRACE = 1, XRT_K_SHADE = 2, XRT_K_FINISH = 3, XRT_K_COUNT = 4 };
+
+typedef struct {
+    double wall_ms;              /* host wall clock of the render call (upload excluded) */
+    double kernel_ms[XRT_K_COUNT];   /* summed HIP-event time per kernel (XRT_FLAG_TIMING) */
+    uint64_t launches[XRT_K_COUNT];  /* launches per kernel                                */
+    uint64_t samples;            /* pixels * spp rendered by this shard                    */
+    uint64_t segments;           /* Scene::intersect calls (extension rays traced)         */
+    uint64_t shadow_rays;        /* Scene::occluded calls                                  */
+    uint64_t draws;              /* RNG draws (Sampler::getNext1D)                         */
+    uint64_t rejected;           /* samples dropped by the NaN/Inf/negative check          */
+    uint64_t iterations;         /* trace+shade pass pairs                                 */
+    uint64_t path_slots;         /* slots in flight (pixels of this shard)                 */
+    uint64_t trace_slot_visits;  /* sum over trace launches of active slots                */
+    uint64_t stalled;            /* paths stopped by the VPT no-progress guard             */
+} xrt_stats;
+
+/* ---- context ----------------------------------------------------------------------- */
+typedef struct xrt_ctx xrt_ctx;
+
+int  xrt_abi_version(void);
+/* device = HIP device ordinal (one process per GPU: LOCAL_RANK) */
+int  xrt_create(int device, xrt_ctx** out);
+void xrt_destroy(xrt_ctx* ctx);
+const char* xrt_last_error(const xrt_ctx* ctx);   /* ctx may be NULL (create failure) */
+
+int  xrt_upload_scene(xrt_ctx* ctx, const xrt_scene_desc* scene);
+/* Camera::camera2world (row-major, row-vector convention, Src/geometry.h:486-498),
+ * PinholeCamera::scale = tan(0.5*deg2rad(FOV)) and aspect_ratio (Src/camera.h:37-47) */
+int  xrt_set_camera(xrt_ctx* ctx, const float c2w[16], float scale, float aspect);
+int  xrt_set_medium(xrt_ctx* ctx, const xrt_medium_desc* medium);
+
+/* Render into caller-owned HOST memory rgb_out[height][width][3] (Image::pixels order
+ * j + width*i).  Pixels outside this shard are written as 0.  Blocks until done. */
+int  xrt_render(xrt_ctx* ctx, const xrt_render_params* p, float* rgb_out, xrt_stats* st);
+/* Same, writing into a DEVICE pointer on this context's GPU (e.g. a torch tensor), so a
+ * multi-GPU caller can reduce framebuffers over RCCL without a host round trip. */
+int  xrt_render_device(xrt_ctx* ctx, const xrt_render_params* p, float* d_rgb_out, xrt_stats* st);
+
+/* ---- host scene layer (C facade over the C++ Scene API; no GPU needed) ------------- */
+typedef struct xrt_hscene xrt_hscene;
+xrt_hscene* xrt_hscene_create(void);
+void xrt_hscene_destroy(xrt_hscene* s);
+const char* xrt_hscene_last_error(const xrt_hscene* s);
+/* Scene::loadObj (Src/scene.cpp:46-154): OBJ/MTL with tinyobjloader-v2 semantics */
+int xrt_hscene_load_obj(xrt_hscene* s, const char* path);
+/* Scene::addObj(name, make_unique<Mesh>(prims, Lambert(albedo))); tri_n may be NULL
+ * (face normals, as loadObj does when the OBJ has no vn) */
+int xrt_hscene_add_mesh(xrt_hscene* s, const char* name, const float* tri_v, const float* tri_n,
+                        uint32_t n_tris, const float albedo[3]);
+/* SphereMesh(center, radius, nTheta, nPhi, Lambert(albedo)) (Src/primitive.cpp:170-205) */
+int xrt_hscene_add_sphere_mesh(xrt_hscene* s, const char* name, const float center[3], float radius,
+                               int n_theta, int n_phi, const float albedo[3]);
+/* Sphere(center, radius, Lambert(albedo)) (Src/primitive.h:97-184) */
+int xrt_hscene_add_sphere(xrt_hscene* s, const char* name, const float center[3], float radius,
+                          const float albedo[3]);
+/* Scene::addAreaLight(name, QuadLight/TriangleLight/SphereLight(..., Matrix44f(), Le)) */
+int xrt_hscene_add_quad_light(xrt_hscene* s, const char* name, const float v0[3], const float v1[3],
+                              const float v2[3], const float Le[3]);
+int xrt_hscene_add_triangle_light(xrt_hscene* s, const char* name, const float v0[3],
+                                  const float v1[3], const float v2[3], const float Le[3]);
+int xrt_hscene_add_sphere_light(xrt_hscene* s, const char* name, const float center[3], float radius,
+                                const float Le[3]);
+/* Scene::addObj(name, medium->makeObject()): a BoxMesh over the medium's bounds */
+int xrt_hscene_add_medium_box(xrt_hscene* s, const char* name, const float pmin[3], const float pmax[3]);
+/* Flatten in unordered_map iteration order.  Pointers stay valid until the next
+ * mutation or destroy. */
+int xrt_hscene_flatten(xrt_hscene* s, xrt_scene_desc* out);
+/* Name of the i-th object in iteration order (NULL if out of range). */
+const char* xrt_hscene_object_name(const xrt_hscene* s, uint32_t i);
+
+/* PinholeCamera(aspect, c2w, FOV) -> scale = tan(0.5f*deg2rad(FOV)) (Src/camera.h:45) */
+float xrt_pinhole_scale(float fov_deg);
+
+/* ---- device self-tests (used by tests/, never by render) ------------------------- */
+/* libstdc++ mt19937 + generate_canonical<float,24> draws for seeds[i], n draws each,
+ * taken at stream offset `skip`: out[i*n + k] */
+int xrt_test_rng(xrt_ctx* ctx, const uint32_t* seeds, uint32_t n_seeds, uint32_t skip, uint32_t n,
+                 float* out);
+/* glibc-sinf/cosf restatement on device over x[i]: out[2i] = sinf, out[2i+1] = cosf */
+int xrt_test_trig(xrt_ctx* ctx, const float* x, uint32_t n, float* out);
+/* exhaustive: count φ = 2π·r over every reachable draw value r where the device
+ * restatement differs from the host values supplied by the caller in chunks. */
+int xrt_test_trig_draw_domain(xrt_ctx* ctx, uint32_t first_bits, uint32_t count, float* out_sin,
+                              float* out_cos, float* out_r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XRT_H */

@@ -1,0 +1,141 @@
+"""ctypes binding of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, __graft_entry__.smoke() (as the checker) and bench.py's
+cpu_baseline leg.  Scene descriptions are the same xrt_scene_desc structs the product
+consumes (xraytracer_amd.abi).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from xraytracer_amd import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+
+class OrcMT(C.Structure):
+    _fields_ = [("x", C.c_uint32 * 624), ("p", C.c_uint32), ("draws", C.c_uint64)]
+
+
+class OrcCamera(C.Structure):
+    _fields_ = [("c2w", C.c_float * 16), ("scale", C.c_float), ("aspect", C.c_float)]
+
+
+class OrcStats(C.Structure):
+    _fields_ = [(k, C.c_uint64) for k in
+                ("samples", "segments", "shadow_rays", "draws", "rejected", "tri_tests", "stalled", "ub_channel")]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+f32p = C.POINTER(C.c_float)
+u32p = C.POINTER(C.c_uint32)
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        l = C.CDLL(LIB)
+        l.orc_mt_seed.argtypes = [C.POINTER(OrcMT), C.c_uint32]
+        l.orc_draw.argtypes = [C.POINTER(OrcMT)]
+        l.orc_draw.restype = C.c_float
+        l.orc_draws.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, f32p]
+        l.orc_render.argtypes = [C.POINTER(abi.XrtSceneDesc), C.POINTER(OrcCamera), C.POINTER(abi.XrtMediumDesc),
+                                 C.POINTER(abi.XrtRenderParams), f32p, C.c_int, C.POINTER(OrcStats)]
+        l.orc_trace_pixels.argtypes = [C.POINTER(abi.XrtSceneDesc), C.POINTER(OrcCamera),
+                                       C.POINTER(abi.XrtMediumDesc), C.POINTER(abi.XrtRenderParams),
+                                       u32p, u32p, C.c_uint32, f32p, u32p, u32p]
+        l.orc_kat_normalize.argtypes = [f32p, f32p]
+        l.orc_kat_onb.argtypes = [f32p, f32p, f32p]
+        l.orc_kat_lambert.argtypes = [C.POINTER(OrcMT), f32p, f32p, f32p, f32p, f32p]
+        l.orc_kat_ray_tri.argtypes = [f32p] * 5 + [f32p]
+        l.orc_kat_sphere.argtypes = [f32p, f32p, f32p, C.c_float, f32p]
+        l.orc_kat_sphere_occluded.argtypes = [f32p, f32p, f32p, C.c_float, C.c_float]
+        l.orc_kat_box.argtypes = [f32p, f32p, f32p, f32p, f32p]
+        l.orc_kat_hg.argtypes = [C.POINTER(OrcMT), C.c_float, f32p, f32p]
+        l.orc_kat_hg.restype = C.c_float
+        l.orc_kat_wavelength.argtypes = [C.POINTER(OrcMT), f32p, f32p, f32p]
+        l.orc_kat_wavelength.restype = C.c_uint32
+        l.orc_kat_light.argtypes = [C.POINTER(OrcMT), C.POINTER(abi.XrtLight), f32p, f32p]
+        _lib = l
+    return _lib
+
+
+def fp(a):
+    return a.ctypes.data_as(f32p)
+
+
+def camera(cam) -> OrcCamera:
+    c = OrcCamera()
+    for i in range(16):
+        c.c2w[i] = float(cam.c2w[i])
+    c.scale = cam.scale
+    c.aspect = cam.aspect
+    return c
+
+
+def params(scene, width, height, spp, shard_index=0, shard_count=1, integrator=None, max_depth=None):
+    p = abi.XrtRenderParams()
+    p.integrator = abi.INTEGRATORS[integrator or scene.integrator]
+    p.max_depth = scene.max_depth if max_depth is None else max_depth
+    p.width, p.height, p.spp = width, height, spp
+    p.shard_index, p.shard_count = shard_index, shard_count
+    return p
+
+
+def render(scene, width, height, spp, nthreads=0, **kw):
+    """NormalRenderer::render restated on the CPU: returns ((H,W,3) float32, stats dict)."""
+    p = params(scene, width, height, spp, **kw)
+    img = np.zeros((height, width, 3), np.float32)
+    st = OrcStats()
+    med = scene.medium.desc() if scene.medium is not None else None
+    rc = lib().orc_render(C.byref(scene.desc), C.byref(camera(scene.camera)),
+                          C.byref(med) if med is not None else None, C.byref(p), fp(img), int(nthreads),
+                          C.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"orc_render failed ({rc})")
+    return img, st.as_dict()
+
+
+def trace_pixels(scene, width, height, spp, pixels, **kw):
+    """Per-sample radiance / draws / Scene::intersect count for pixels [(i, j), ...]."""
+    p = params(scene, width, height, spp, **kw)
+    pi = np.ascontiguousarray([q[0] for q in pixels], dtype=np.uint32)
+    pj = np.ascontiguousarray([q[1] for q in pixels], dtype=np.uint32)
+    n = len(pixels)
+    rad = np.zeros((n, spp, 3), np.float32)
+    dr = np.zeros((n, spp), np.uint32)
+    sg = np.zeros((n, spp), np.uint32)
+    med = scene.medium.desc() if scene.medium is not None else None
+    rc = lib().orc_trace_pixels(C.byref(scene.desc), C.byref(camera(scene.camera)),
+                                C.byref(med) if med is not None else None, C.byref(p),
+                                pi.ctypes.data_as(u32p), pj.ctypes.data_as(u32p), n, fp(rad),
+                                dr.ctypes.data_as(u32p), sg.ctypes.data_as(u32p))
+    if rc != 0:
+        raise RuntimeError(f"orc_trace_pixels failed ({rc})")
+    return rad, dr, sg
+
+
+def draws(seed, n, skip=0):
+    out = np.zeros(n, np.float32)
+    lib().orc_draws(seed, skip, n, fp(out))
+    return out
+
+
+def mt(seed) -> OrcMT:
+    m = OrcMT()
+    lib().orc_mt_seed(C.byref(m), seed)
+    return m

@@ -1,0 +1,272 @@
+// ref_kats.cpp — known-answer vectors from the REFERENCE's own code, compiled in place.
+//
+// TEST INFRASTRUCTURE ONLY.  Built by `make -C oracle ref` from
+//   /root/reference/Src/geometry.cpp, /root/reference/Src/sampler.cpp and this driver,
+// which includes the reference headers geometry.h, sampler.h, ray.h, primitive.h,
+// material.h and medium.h unmodified (-I /root/reference/Src).  Only the compile
+// definitions of Src/cmakelists.txt:57-65 (kEpsilon, kInfinity) and `-include cfloat`
+// (for FLT_EPSILON / FLT_MAX, which the MSVC headers of the original build make visible
+// transitively) are added.  No reference source is copied; no stand-in headers are used.
+// Translation units that need spdlog / OpenCV / OpenVDB / tinyobjloader (camera.h,
+// light.*, primitive.cpp, scene.*, integrator.h, renderer.*, medium.cpp, grid.h) are
+// NOT buildable here and are not used.
+//
+// Output: one JSON object on stdout; every float is emitted as its uint32 bit pattern.
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "geometry.h"
+#include "material.h"
+#include "medium.h"
+#include "primitive.h"
+#include "ray.h"
+#include "sampler.h"
+
+namespace {
+
+uint32_t bits(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+}
+
+// deterministic input generator (xorshift32) — inputs are emitted with the outputs
+struct Gen {
+    uint32_t s;
+    explicit Gen(uint32_t seed) : s(seed) {}
+    uint32_t next() {
+        s ^= s << 13;
+        s ^= s >> 17;
+        s ^= s << 5;
+        return s;
+    }
+    float uni(float a, float b) { return a + (b - a) * (float)(next() >> 8) * (1.0f / 16777216.0f); }
+    Vec3f vec(float a, float b) {
+        float x = uni(a, b), y = uni(a, b), z = uni(a, b);
+        return Vec3f(x, y, z);
+    }
+};
+
+struct Out {
+    std::string s;
+    bool first = true;
+    void key(const char* k) {
+        s += first ? "" : ",\n";
+        first = false;
+        s += "\"";
+        s += k;
+        s += "\": ";
+    }
+    void arr(const std::vector<uint32_t>& v) {
+        s += "[";
+        for (size_t i = 0; i < v.size(); ++i) {
+            if (i) s += ",";
+            s += std::to_string(v[i]);
+        }
+        s += "]";
+    }
+};
+
+void push3(std::vector<uint32_t>& v, const Vec3f& a) {
+    v.push_back(bits(a[0]));
+    v.push_back(bits(a[1]));
+    v.push_back(bits(a[2]));
+}
+
+}  // namespace
+
+int main() {
+    Out o;
+    o.s = "{\n";
+
+    // 1. UniformSampler streams (Src/sampler.h:37-50, 25): seeds and 2000 draws each,
+    //    plus draws 100000..100099 of seed 7 (several twists deep).
+    {
+        const uint32_t seeds[] = {0u, 1u, 255u, 65535u, 479999u, 2073599u, 4294967295u};
+        std::vector<uint32_t> sv, dv;
+        for (uint32_t sd : seeds) {
+            UniformSampler smp;
+            smp.setSeed(sd);
+            sv.push_back(sd);
+            for (int k = 0; k < 2000; ++k) dv.push_back(bits(smp.getNext1D()));
+        }
+        o.key("rng_seeds"); o.arr(sv);
+        o.key("rng_draws_2000"); o.arr(dv);
+        UniformSampler smp;
+        smp.setSeed(7);
+        for (int k = 0; k < 100000; ++k) smp.getNext1D();
+        std::vector<uint32_t> deep;
+        for (int k = 0; k < 100; ++k) deep.push_back(bits(smp.getNext1D()));
+        o.key("rng_seed7_skip100000"); o.arr(deep);
+        // getNext2D order (Src/sampler.h:49): Vec2f(dis(gen), dis(gen))
+        UniformSampler s2;
+        s2.setSeed(12345);
+        std::vector<uint32_t> v2;
+        for (int k = 0; k < 64; ++k) {
+            Vec2f u = s2.getNext2D();
+            v2.push_back(bits(u[0]));
+            v2.push_back(bits(u[1]));
+        }
+        o.key("rng_seed12345_next2d"); o.arr(v2);
+    }
+
+    // 2. normalize + orthonormalBasis (Src/geometry.cpp:13-16, 43-49)
+    {
+        Gen g(0x1234567u);
+        std::vector<uint32_t> in, nrm, t, b;
+        for (int k = 0; k < 512; ++k) {
+            Vec3f v = g.vec(-3.0f, 3.0f);
+            if (k % 7 == 0) v[2] = 0.0f;  // copysign(1, +0) branch
+            push3(in, v);
+            Vec3f n = normalize(v);
+            push3(nrm, n);
+            Vec3f tt, bb;
+            orthonormalBasis(n, tt, bb);
+            push3(t, tt);
+            push3(b, bb);
+        }
+        o.key("onb_in"); o.arr(in);
+        o.key("onb_normalized"); o.arr(nrm);
+        o.key("onb_t"); o.arr(t);
+        o.key("onb_b"); o.arr(b);
+    }
+
+    // 3. Lambert::sampleDir (Src/material.h:55-73) — SurfaceInfo with ng and the ONB of ng
+    {
+        Gen g(0xBADC0DEu);
+        Lambert lam(Vec3f(0.5f, 0.25f, 1.0f));
+        UniformSampler smp;
+        smp.setSeed(2024);
+        std::vector<uint32_t> in, wi, pdfs;
+        for (int k = 0; k < 512; ++k) {
+            SurfaceInfo si;
+            si.ng = normalize(g.vec(-1.0f, 1.0f));
+            orthonormalBasis(si.ng, si.dpdu, si.dpdv);
+            push3(in, si.ng);
+            push3(in, si.dpdu);
+            push3(in, si.dpdv);
+            float pdf = 0.0f;
+            Vec3f w = lam.sampleDir(si, smp, pdf);
+            push3(wi, w);
+            pdfs.push_back(bits(pdf));
+        }
+        o.key("lambert_seed"); o.arr({2024u});
+        o.key("lambert_in"); o.arr(in);
+        o.key("lambert_wi"); o.arr(wi);
+        o.key("lambert_pdf"); o.arr(pdfs);
+    }
+
+    // 4. Sphere::intersect / occluded (Src/primitive.h:106-156): rays aimed near spheres
+    {
+        Gen g(0x5EEDu);
+        std::vector<uint32_t> in, hit, out, occ;
+        for (int k = 0; k < 1024; ++k) {
+            Vec3f c = g.vec(-20.0f, 20.0f);
+            float r = g.uni(0.1f, 5.0f);
+            Vec3f orig = g.vec(-30.0f, 30.0f);
+            if (k % 5 == 0) orig = c + g.vec(-0.5f, 0.5f) * r;  // start inside
+            Vec3f target = c + g.vec(-1.5f, 1.5f) * r;
+            Vec3f dir = normalize(target - orig);
+            if (k % 3 == 0) dir = dir * g.uni(0.5f, 2.0f);     // non-unit direction
+            float tmax = g.uni(0.0f, 60.0f);
+            push3(in, orig);
+            push3(in, dir);
+            push3(in, c);
+            in.push_back(bits(r));
+            in.push_back(bits(tmax));
+            Sphere sp(c, r, nullptr, nullptr);
+            Ray ray(orig, dir);
+            IntersectInfo info;
+            bool h = sp.intersect(ray, info);
+            hit.push_back(h ? 1u : 0u);
+            out.push_back(bits(info.t));
+            push3(out, info.surfaceInfo.position);
+            push3(out, info.surfaceInfo.ng);
+            occ.push_back(sp.occluded(ray, tmax) ? 1u : 0u);
+        }
+        o.key("sphere_in"); o.arr(in);
+        o.key("sphere_hit"); o.arr(hit);
+        o.key("sphere_out"); o.arr(out);
+        o.key("sphere_occluded"); o.arr(occ);
+    }
+
+    // 5. BoxMesh::intersect (Src/primitive.h:243-264)
+    {
+        Gen g(0xB0B0u);
+        std::vector<uint32_t> in, hit, out;
+        for (int k = 0; k < 1024; ++k) {
+            Vec3f a = g.vec(-10.0f, 10.0f), b = g.vec(-10.0f, 10.0f);
+            AABB box{vmin(a, b), vmax(a, b)};
+            Vec3f orig = g.vec(-20.0f, 20.0f);
+            Vec3f dir = normalize(g.vec(-1.0f, 1.0f));
+            if (k % 9 == 0) dir[k % 3] = 0.0f;  // axis-parallel: 1/0 = inf slabs
+            push3(in, orig);
+            push3(in, dir);
+            push3(in, box.pMin);
+            push3(in, box.pMax);
+            BoxMesh bm(box, nullptr);
+            IntersectInfo info;
+            bool h = bm.intersect(Ray(orig, dir), info);
+            hit.push_back(h ? 1u : 0u);
+            out.push_back(bits(info.t));
+            out.push_back(bits(info.t1));
+        }
+        o.key("box_in"); o.arr(in);
+        o.key("box_hit"); o.arr(hit);
+        o.key("box_out"); o.arr(out);
+    }
+
+    // 6. HenyeyGreenstein::sampleDirection / evaluate (Src/medium.h:21-68)
+    {
+        const float gs[] = {0.0f, 0.0005f, 0.5f, -0.3f, 0.85f};
+        Gen g(0x4E4Eu);
+        std::vector<uint32_t> gv, in, wi, val;
+        for (float gg : gs) {
+            HenyeyGreenstein hg(gg);
+            UniformSampler smp;
+            smp.setSeed(99);
+            gv.push_back(bits(gg));
+            for (int k = 0; k < 256; ++k) {
+                Vec3f wo = normalize(g.vec(-1.0f, 1.0f));
+                push3(in, wo);
+                Vec3f w;
+                float v = hg.sampleDirection(wo, smp, w);
+                push3(wi, w);
+                val.push_back(bits(v));
+            }
+        }
+        o.key("hg_g"); o.arr(gv);
+        o.key("hg_seed"); o.arr({99u});
+        o.key("hg_wo"); o.arr(in);
+        o.key("hg_wi"); o.arr(wi);
+        o.key("hg_eval"); o.arr(val);
+    }
+
+    // 7. Medium::sampleWavelength (Src/medium.h:102-115) + DiscreteEmpiricalDistribution1D
+    {
+        Gen g(0xC0C0u);
+        UniformSampler smp;
+        smp.setSeed(4242);
+        std::vector<uint32_t> in, ch, pmf;
+        for (int k = 0; k < 1024; ++k) {
+            Vec3f thr = g.vec(0.0f, 2.0f), alb = g.vec(0.0f, 1.0f);
+            if (k % 11 == 0) thr[k % 3] = 0.0f;
+            push3(in, thr);
+            push3(in, alb);
+            Vec3f p;
+            ch.push_back(Medium::sampleWavelength(thr, alb, smp, p));
+            push3(pmf, p);
+        }
+        o.key("wl_seed"); o.arr({4242u});
+        o.key("wl_in"); o.arr(in);
+        o.key("wl_channel"); o.arr(ch);
+        o.key("wl_pmf"); o.arr(pmf);
+    }
+
+    o.s += "\n}\n";
+    std::fputs(o.s.c_str(), stdout);
+    return 0;
+}

@@ -1,0 +1,20 @@
+// launch.h — host-callable kernel launchers (defined in wavefront.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "wavefront.h"
+
+namespace xrt {
+hipError_t launch_seed(const KParams& P, uint32_t* list, uint32_t* count, uint32_t* count_other, hipStream_t st);
+hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
+                        uint32_t blocks, hipStream_t st);
+hipError_t launch_shade(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
+                        uint32_t* out_count, uint32_t blocks, hipStream_t st);
+hipError_t launch_finish(const KParams& P, hipStream_t st);
+hipError_t launch_test_rng(const uint32_t* seeds, uint32_t n_seeds, uint32_t skip, uint32_t n, float* out,
+                           uint32_t* rings, hipStream_t st);
+hipError_t launch_test_trig(const float* x, uint32_t n, float* out, hipStream_t st);
+hipError_t launch_test_trig_domain(uint32_t first, uint32_t count, float* s, float* c, float* r, hipStream_t st);
+}  // namespace xrt

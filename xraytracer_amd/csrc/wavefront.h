@@ -1,0 +1,105 @@
+// wavefront.h — device data layout of the MI355X wavefront path tracer, shared by the
+// kernels (wavefront.hip) and the host orchestration (xrt_api.cpp).
+//
+// HBM layout (DESIGN.md §Data layout):
+//   scene  : triangles as 3 float4 per triangle {(v0, obj), (e1 = v1-v0, occluder), (e2 = v2-v0, 0)}
+//            in Scene::m_objects order, plus per-triangle ng and vertex normals read only
+//            at shading; spheres {(c, r)}; boxes {pmin, pmax}; object and light tables.
+//   slots  : one path slot per pixel of this shard; all per-slot state is SoA (float4 /
+//            uint32 arrays indexed by slot) so a wave's loads are coalesced.
+//   RNG    : per slot a 1248-word ring (two 624-word mt19937 blocks) + cursor/generated
+//            counters; refilled one 624-word twist at a time by a whole wave.
+#pragma once
+#include <stdint.h>
+
+#ifndef __HIPCC__
+struct float4_ { float x, y, z, w; };
+#endif
+
+namespace xrt {
+
+constexpr int kMaxLights = 4;        // shadow rays in flight per slot (one per area light)
+constexpr uint32_t kMT = 624;        // mt19937 state words
+constexpr uint32_t kRing = 1248;     // ring words per slot
+constexpr uint32_t kRngMin = 64;     // refill when fewer draws than this remain
+
+// slot state bits
+enum : uint32_t {
+    ST_RAY = 1u,      // extension ray pending (shade -> trace) / hit record valid (trace -> shade)
+    ST_NEE = 2u,      // NEE contributions pending resolution (after the shadow rays are traced)
+    ST_END = 4u,      // path ends after the NEE resolve
+    ST_REGEN = 8u,    // slot must start its next sample
+    ST_DONE = 16u,    // all samples of this pixel are done
+    ST_MEDIUM = 32u,  // VPT delta-tracking loop suspended (resumes after an RNG refill)
+    ST_SHADOW_SHIFT = 8u  // bits 8..15: which lights have a shadow ray in flight
+};
+
+enum : int { SEG_TRI = 0, SEG_SPHERE = 1, SEG_BOX = 2 };
+enum : int { SCN_TRI = 0, SCN_SPHERE = 1, SCN_MIXED = 2 };  // trace kernel specialisations
+
+struct DSeg {   // a run of consecutive objects of one kind, in iteration order
+    int kind, first, count, pad;
+};
+
+struct DObj {
+    int kind, material, light, medium;
+    float albedo[3];
+    float pad;
+};
+
+struct DLight {  // e1/e2/Ng precomputed on the host with the reference constructor's ops
+    int kind;
+    float v0[3], v1[3], v2[3], e1[3], e2[3], Ng[3], center[3], radius, Le[3];
+};
+
+struct DMedium {
+    const float* density;  // [nz][ny][nx]
+    int nx, ny, nz;
+    float origin[3], voxel_size;
+    float absorption[3], scattering[3], multiplier, g;
+    float majorant, inv_majorant;
+};
+
+#ifdef __HIPCC__
+using f4 = float4;
+#else
+using f4 = float4_;
+#endif
+
+struct KParams {
+    // ---- scene
+    const f4* tri;      // [3 * n_tris]
+    const f4* tri_ng;   // [n_tris]
+    const f4* tri_nrm;  // [3 * n_tris]
+    const f4* sph;      // [n_sph] (center, radius)
+    const int* sph_obj; // [n_sph] object index; bit 30 set = occluder
+    const f4* box;      // [2 * n_box] (pmin, obj) (pmax, 0)
+    const DObj* objs;
+    const DLight* lights;
+    const DSeg* segs;
+    int n_segs, n_lights, n_tris, n_sph, n_box, scene_kind;
+    DMedium medium;
+    // ---- camera (row-major c2w) + PinholeCamera scale / aspect
+    float c2w[16];
+    float scale, aspect;
+    // ---- render
+    int integrator;
+    uint32_t max_depth, width, height, spp, shard_index, shard_count, n_slots;
+    // ---- slot state (SoA)
+    f4 *ray_o, *ray_d, *thr, *rad, *thr_prev;
+    f4 *hit;     // t, u, v, code(bits)        code: -1 miss, (kind << 28) | prim
+    f4 *hit2;    // t1, surf code, dp code, surf t   (mixed scenes / boxes)
+    f4 *hit3;    // surf u, surf v, dp u, dp v
+    f4 *sh_o;    // [kMaxLights][n_slots] origin, tmax
+    f4 *sh_d;    // [kMaxLights][n_slots] direction
+    f4 *sh_c;    // [kMaxLights][n_slots] unoccluded contribution
+    f4 *med;     // VPT suspended delta-tracking state: t, t1, ...
+    f4 *med2;
+    uint32_t *state, *sample_k, *depth, *occ;
+    uint32_t *rng_c, *rng_g, *ring;
+    uint32_t *c_seg, *c_shadow, *c_rej, *c_stall;
+    float* fb;                 // [height][width][3]
+    unsigned long long* stats; // device reduction target: seg, shadow, draws, rej, stall
+};
+
+}  // namespace xrt

@@ -1,0 +1,867 @@
+// wavefront.hip — gfx950 kernels of the wavefront path tracer.
+//
+// One path slot per pixel of the shard.  Each iteration runs two passes over a compacted
+// slot list:
+//   k_shade : per slot — resolve last bounce's NEE (shadow results), shade the hit record
+//             (RR, emitter, NEE light samples -> shadow rays, Lambert BSDF sample ->
+//             extension ray), finalize a finished sample into the framebuffer and
+//             regenerate the pixel's next camera ray; ballot/prefix-sum compaction of the
+//             slots that still have rays to trace.
+//   k_trace : closest-hit for extension rays and any-hit for shadow rays over the linear
+//             primitive array, staged through LDS in tiles shared by the block's rays.
+// Per-pixel RNG is an exact restatement of the reference's std::mt19937 stream; a pixel's
+// samples run in order (sample k+1 starts in the same k_shade call that finalises k), so
+// every pixel consumes its stream exactly as NormalRenderer::doRender does
+// (Src/renderer.cpp:29-81).
+#include <hip/hip_runtime.h>
+
+#include "device_math.h"
+#include "wavefront.h"
+#include "xrt.h"
+
+namespace xrt {
+
+constexpr int kBlock = 256;
+constexpr int kTriTile = 512;    // triangles per LDS tile (24 KiB)
+constexpr int kSphTile = 1024;   // spheres per LDS tile (16 KiB + 4 KiB)
+
+// ============================================================================ RNG ====
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+// generate_canonical<float,24>: (float)x / 2^32, nextafter(1,0) if it rounds to 1
+__device__ __forceinline__ float canonical(uint32_t y) {
+    const float f = (float)y * 0x1p-32f;
+    return f >= 1.0f ? 0x1.fffffep-1f : f;
+}
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+struct Rng {
+    const uint32_t* ring;
+    uint32_t c;
+    __device__ __forceinline__ float next() {
+        const uint32_t y = ring[c % kRing];
+        ++c;
+        return canonical(mt_temper(y));
+    }
+};
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One mt19937 twist of a slot's stream done by a whole wave: x[g+k] = x[g+k-227] ^
+// mix(x[g+k-624], x[g+k-623]) for k = 0..623 (libstdc++ _M_gen_rand), computed in three
+// dependency-free chunks of 227/227/170 words through LDS; the new block lands in ring
+// half g % 1248 over the oldest (fully consumed) block.
+__device__ void wave_twist(uint32_t* ring, uint32_t g, uint32_t* lds, int lane) {
+    const uint32_t h = g % kRing;
+    const uint32_t hp = kMT - h;
+    uint32_t* old = lds;
+    uint32_t* nw = lds + kMT;
+    for (uint32_t i = lane; i < kMT; i += 64) old[i] = ring[hp + i];
+    wave_sync();
+    for (uint32_t k = lane; k < 227; k += 64) nw[k] = old[k + 397] ^ mt_mix(old[k], old[k + 1]);
+    wave_sync();
+    for (uint32_t k = 227 + lane; k < 454; k += 64) nw[k] = nw[k - 227] ^ mt_mix(old[k], old[k + 1]);
+    wave_sync();
+    for (uint32_t k = 454 + lane; k < kMT; k += 64)
+        nw[k] = nw[k - 227] ^ mt_mix(old[k], k < kMT - 1 ? old[k + 1] : nw[0]);
+    wave_sync();
+    for (uint32_t i = lane; i < kMT; i += 64) ring[h + i] = nw[i];
+    wave_sync();
+}
+
+// Must be called by every lane of the wave (wave-uniform control flow).
+__device__ void wave_refill(bool need, uint32_t slot, uint32_t& g, uint32_t* rings, uint32_t* lds, int lane) {
+    uint64_t m = __ballot(need);
+    if (m == 0) return;
+    while (m) {
+        const int L = __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        const uint32_t sl = __shfl(slot, L);
+        const uint32_t gl = __shfl(g, L);
+        wave_twist(rings + (size_t)sl * kRing, gl, lds, lane);
+    }
+    if (need) g += kMT;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
+
+// ====================================================================== geometry ====
+// Mesh::rayTriangleIntersect, no CULLING (Src/primitive.cpp:140-168), with e1 = v1 - v0,
+// e2 = v2 - v0 precomputed on the host by the same subtraction.
+__device__ __forceinline__ bool ray_tri(v3 o, v3 d, v3 v0, v3 e1, v3 e2, float& t, float& u, float& v) {
+    const v3 pvec = cross(d, e2);
+    const float det = dot(e1, pvec);
+    if (__builtin_fabsf(det) < kEPSILON) return false;
+    const float invDet = 1.0f / det;
+    const v3 tvec = o - v0;
+    u = dot(tvec, pvec) * invDet;
+    if (u < 0.0f || u > 1.0f) return false;
+    const v3 qvec = cross(tvec, e1);
+    v = dot(d, qvec) * invDet;
+    if (v < 0.0f || u + v > 1.0f) return false;
+    t = dot(e2, qvec) * invDet;
+    return t > kEPSILON;
+}
+
+// Sphere::doIntersect + solveQuadratic (Src/primitive.h:133-177): double -0.5*(b±sqrt)
+__device__ __forceinline__ bool sphere_hit(v3 o, v3 d, v3 c, float r, float& tnear) {
+    const v3 L = o - c;
+    const float a = dot(d, d);
+    const float b = 2.0f * dot(d, L);
+    const float cc = dot(L, L) - r * r;
+    const float discr = b * b - 4.0f * a * cc;
+    if (discr < 0.0f) return false;
+    float t0, t1;
+    if (discr == 0.0f) {
+        t0 = t1 = (float)(-0.5 * (double)b / (double)a);
+    } else {
+        const double sq = __builtin_sqrt((double)discr);
+        const float q = (b > 0.0f) ? (float)(-0.5 * ((double)b + sq)) : (float)(-0.5 * ((double)b - sq));
+        t0 = q / a;
+        t1 = cc / q;
+    }
+    if (t0 > t1) { const float tmp = t0; t0 = t1; t1 = tmp; }
+    if (t0 < 0.0f) {
+        t0 = t1;
+        if (t0 < 0.0f) return false;
+    }
+    tnear = t0;
+    return true;
+}
+
+// BoxMesh::intersect slab test (Src/primitive.h:243-264)
+__device__ __forceinline__ bool box_hit(v3 o, v3 d, v3 pmin, v3 pmax, float& t0, float& t1) {
+    const v3 di = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const v3 tt = di * (pmax - o), tb = di * (pmin - o);
+    const v3 tmin = mk(smin(tt.x, tb.x), smin(tt.y, tb.y), smin(tt.z, tb.z));
+    const v3 tmax = mk(smax(tt.x, tb.x), smax(tt.y, tb.y), smax(tt.z, tb.z));
+    t0 = smax(smax(tmin.x, tmin.y), tmin.z);
+    t1 = smin(smin(tmax.x, tmax.y), tmax.z);
+    if (t0 > t1 || t1 <= 0.0f) return false;
+    t0 = smax(t0, 0.0f);
+    return true;
+}
+
+// ==================================================================== k_seed ====
+// mt19937::seed(j + width*i) for every slot (Src/renderer.cpp:35-36).  The recurrence is
+// serial per pixel, so each lane runs one pixel's recurrence and the wave writes the words
+// out through an LDS transpose (64 pixels x 64 words, padded row) as coalesced 256-B rows.
+__global__ __launch_bounds__(kBlock) void k_seed(KParams P, uint32_t* list, uint32_t* count, uint32_t* count_other) {
+    __shared__ uint32_t lds[4][64][65];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t base = (blockIdx.x * kBlock) + wv * 64;
+    const uint32_t s = base + lane;
+    const bool valid = s < P.n_slots;
+    uint32_t row = 0, col = 0;
+    if (valid) {
+        col = s % P.width;
+        row = P.shard_index + P.shard_count * (s / P.width);
+    }
+    uint32_t x = col + P.width * row;  // seed j + width * i
+    for (uint32_t q = 0; q < kMT; q += 64) {
+        for (uint32_t j = 0; j < 64; ++j) {
+            const uint32_t i = q + j;
+            if (i > 0 && i < kMT) x = 1812433253u * (x ^ (x >> 30)) + i;
+            lds[wv][lane][j] = x;
+        }
+        wave_sync();
+        for (uint32_t r = 0; r < 64; ++r) {
+            const uint32_t sl = base + r;
+            if (sl < P.n_slots && q + lane < kMT) P.ring[(size_t)sl * kRing + q + lane] = lds[wv][r][lane];
+        }
+        wave_sync();
+    }
+    if (valid) {
+        P.rng_c[s] = kMT;   // cursor: next output is x[624]
+        P.rng_g[s] = kMT;   // generated: x[0..623]
+        P.state[s] = ST_REGEN;
+        P.sample_k[s] = 0;
+        P.depth[s] = 0;
+        P.occ[s] = 0;
+        P.c_seg[s] = 0;
+        P.c_shadow[s] = 0;
+        P.c_rej[s] = 0;
+        P.c_stall[s] = 0;
+        list[s] = s;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *count = P.n_slots;
+        *count_other = 0;
+    }
+}
+
+// =================================================================== k_trace ====
+template <int SCN, int NL>
+__global__ __launch_bounds__(kBlock) void k_trace(KParams P, const uint32_t* __restrict__ list,
+                                                   const uint32_t* __restrict__ count, uint32_t* zero_count) {
+    __shared__ f4 lds_tri[SCN == SCN_SPHERE ? 1 : 3 * kTriTile];
+    __shared__ f4 lds_sph[SCN == SCN_TRI ? 1 : kSphTile];
+    __shared__ int lds_sobj[SCN == SCN_TRI ? 1 : kSphTile];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *zero_count = 0;
+    const uint32_t n = *count;
+    const int tid = threadIdx.x;
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const uint32_t i = base + tid;
+        const bool valid = i < n;
+        const uint32_t s = valid ? list[i] : 0;
+        const uint32_t st = valid ? P.state[s] : 0;
+        const bool want = (st & ST_RAY) != 0;
+        const uint32_t smask = (st >> ST_SHADOW_SHIFT) & ((1u << NL) - 1u);
+        v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+        if (want) {
+            o = xyz(P.ray_o[s]);
+            d = xyz(P.ray_d[s]);
+        }
+        v3 so[NL], sd[NL];
+        float stmax[NL];
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+            so[l] = mk(0, 0, 0), sd[l] = mk(0, 0, 0), stmax[l] = 0.0f;
+            if (smask & (1u << l)) {
+                const f4 a = P.sh_o[(size_t)l * P.n_slots + s];
+                so[l] = xyz(a);
+                stmax[l] = a.w;
+                sd[l] = xyz(P.sh_d[(size_t)l * P.n_slots + s]);
+            }
+        }
+        uint32_t occ = 0;
+        float best_t = kINF, bu = 0.0f, bv = 0.0f;
+        int best = -1;
+        // mixed scenes: which primitive last wrote SurfaceInfo (position/ng/ns) and which
+        // triangle last wrote dpdu/dpdv (spheres and boxes leave them untouched)
+        int surf = -1, dp = -1;
+        float surf_t = 0.0f, surf_u = 0.0f, surf_v = 0.0f, dp_u = 0.0f, dp_v = 0.0f, t1 = kINF;
+
+        for (int sg = 0; sg < P.n_segs; ++sg) {
+            const DSeg seg = P.segs[sg];
+            if (SCN != SCN_SPHERE && seg.kind == SEG_TRI) {
+                for (int tb = seg.first; tb < seg.first + seg.count; tb += kTriTile) {
+                    const int nt = min(kTriTile, seg.first + seg.count - tb);
+                    __syncthreads();
+                    for (int q = tid; q < 3 * nt; q += kBlock) lds_tri[q] = P.tri[3 * (size_t)tb + q];
+                    __syncthreads();
+                    for (int k = 0; k < nt; ++k) {
+                        const f4 A = lds_tri[3 * k], B = lds_tri[3 * k + 1], Cc = lds_tri[3 * k + 2];
+                        const v3 v0 = xyz(A), e1 = xyz(B), e2 = xyz(Cc);
+                        if (want) {
+                            float t, u, v;
+                            if (ray_tri(o, d, v0, e1, e2, t, u, v) && t < best_t) {
+                                best_t = t, bu = u, bv = v, best = tb + k;
+                                if (SCN == SCN_MIXED) surf = best, surf_t = t, surf_u = u, surf_v = v, dp = best, dp_u = u, dp_v = v;
+                            }
+                        }
+                        if (B.w != 0.0f) {  // occluder (object without an area light)
+#pragma unroll
+                            for (int l = 0; l < NL; ++l) {
+                                if ((smask & (1u << l)) && !(occ & (1u << l))) {
+                                    float t, u, v;
+                                    if (ray_tri(so[l], sd[l], v0, e1, e2, t, u, v) && t < stmax[l]) occ |= 1u << l;
+                                }
+                            }
+                        }
+                    }
+                }
+            } else if (SCN != SCN_TRI && seg.kind == SEG_SPHERE) {
+                for (int tb = seg.first; tb < seg.first + seg.count; tb += kSphTile) {
+                    const int nt = min(kSphTile, seg.first + seg.count - tb);
+                    __syncthreads();
+                    for (int q = tid; q < nt; q += kBlock) {
+                        lds_sph[q] = P.sph[tb + q];
+                        lds_sobj[q] = P.sph_obj[tb + q];
+                    }
+                    __syncthreads();
+                    for (int k = 0; k < nt; ++k) {
+                        const f4 S = lds_sph[k];
+                        const v3 c = xyz(S);
+                        if (want) {
+                            float t;
+                            if (sphere_hit(o, d, c, S.w, t) && t < best_t) {
+                                best_t = t, bu = 0.0f, bv = 0.0f, best = (1 << 28) | (tb + k);
+                                if (SCN == SCN_MIXED) surf = best, surf_t = t;
+                            }
+                        }
+                        if (lds_sobj[k] & (1 << 30)) {
+#pragma unroll
+                            for (int l = 0; l < NL; ++l) {
+                                if ((smask & (1u << l)) && !(occ & (1u << l))) {
+                                    float t;
+                                    if (sphere_hit(so[l], sd[l], c, S.w, t) && t < stmax[l]) occ |= 1u << l;
+                                }
+                            }
+                        }
+                    }
+                }
+            } else if (SCN == SCN_MIXED && seg.kind == SEG_BOX) {
+                for (int b = seg.first; b < seg.first + seg.count; ++b) {
+                    const v3 pmin = xyz(P.box[2 * b]), pmax = xyz(P.box[2 * b + 1]);
+                    if (want) {
+                        float t0, tt1;
+                        if (box_hit(o, d, pmin, pmax, t0, tt1)) best_t = t0, t1 = tt1, best = (2 << 28) | b;
+                    }
+                    // BoxMesh::occluded returns true unconditionally (Src/primitive.h:266-268)
+                    occ |= smask;
+                }
+            }
+        }
+        if (valid) {
+            if (want) {
+                P.hit[s] = make_float4(best_t, bu, bv, __int_as_float(best));
+                if (SCN == SCN_MIXED) {
+                    P.hit2[s] = make_float4(t1, __int_as_float(surf), __int_as_float(dp), surf_t);
+                    P.hit3[s] = make_float4(surf_u, surf_v, dp_u, dp_v);
+                }
+            }
+            if (smask) P.occ[s] = occ;
+        }
+    }
+}
+
+// =================================================================== shading ====
+struct Surf {
+    v3 pos, ng, ns, dpdu, dpdv;
+    int obj;
+};
+
+__device__ __forceinline__ v3 tri_ns(const KParams& P, int i, float u, float v) {
+    const float w = 1.0f - u - v;
+    return xyz(P.tri_nrm[3 * i]) * w + xyz(P.tri_nrm[3 * i + 1]) * u + xyz(P.tri_nrm[3 * i + 2]) * v;
+}
+
+// Rebuild IntersectInfo::surfaceInfo as Scene::intersect leaves it (Src/primitive.cpp:
+// 102-110, primitive.h:112-122).  Returns the hit object index (-1 = miss).
+template <int SCN>
+__device__ __forceinline__ int surface(const KParams& P, uint32_t s, v3 o, v3 d, f4 h, Surf& S, float& t1) {
+    const int code = __float_as_int(h.w);
+    S.pos = S.ng = S.ns = S.dpdu = S.dpdv = mk(0, 0, 0);
+    t1 = kINF;
+    if (code < 0) return -1;
+    int surf = code, dp = (SCN == SCN_TRI) ? code : -1;
+    float st = h.x, su = h.y, sv = h.z, du = h.y, dv = h.z;
+    if (SCN == SCN_MIXED) {
+        const f4 h2 = P.hit2[s], h3 = P.hit3[s];
+        t1 = h2.x;
+        surf = __float_as_int(h2.y), dp = __float_as_int(h2.z), st = h2.w;
+        su = h3.x, sv = h3.y, du = h3.z, dv = h3.w;
+    }
+    if (surf >= 0) {
+        const int kind = surf >> 28, idx = surf & 0x0fffffff;
+        S.pos = ray_at(o, d, st);
+        if (kind == SEG_TRI) {
+            S.ng = xyz(P.tri_ng[idx]);
+            S.ns = tri_ns(P, idx, su, sv);
+        } else {
+            S.ng = normalize(ray_at(o, d, st) - xyz(P.sph[idx]));
+            S.ns = S.ng;
+        }
+    }
+    if (dp >= 0) onb(tri_ns(P, dp & 0x0fffffff, du, dv), S.dpdu, S.dpdv);
+    const int kind = code >> 28, idx = code & 0x0fffffff;
+    if (kind == SEG_TRI) return __float_as_int(P.tri[3 * idx].w);
+    if (kind == SEG_SPHERE) return P.sph_obj[idx] & 0x3fffffff;
+    return __float_as_int(P.box[2 * idx].w);
+}
+
+// AreaLight::Le (Src/light.h:62-69)
+__device__ __forceinline__ v3 light_Le(const DLight& L, v3 ns, v3 wi) {
+    return dot(wi, ns) < 0.0f ? mk(L.Le[0], L.Le[1], L.Le[2]) : mk(0, 0, 0);
+}
+
+__device__ __forceinline__ v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+
+// QuadLight::sample (Src/light.cpp:59-68; first draw scales e2 under GCC),
+// TriangleLight::sample (light.cpp:21-30,43-47; first draw is v),
+// SphereLight::sample default branch (light.h:157-197).  pdf is left untouched on the
+// back-facing early return, as in the reference.
+__device__ v3 light_sample(const DLight& L, v3 x, v3& wi, float& pdf, float& tmax, Rng& rng) {
+    if (L.kind == 0) {
+        const float ra = rng.next();
+        const float rb = rng.next();
+        const v3 dd = ((ld3(L.v0) + ld3(L.e1) * rb) + ld3(L.e2) * ra) - x;
+        tmax = length(dd);
+        const float dn = dot(dd, ld3(L.Ng));
+        if (dn >= 0.0f) return mk(0, 0, 0);
+        wi = dd / tmax;
+        pdf = (tmax * tmax * tmax) / __builtin_fabsf(dn);
+        return ld3(L.Le);
+    } else if (L.kind == 1) {
+        const float vv = rng.next();
+        const float uu = rng.next();
+        const float su = __builtin_sqrtf(uu);
+        const v3 A = ld3(L.v0), B = ld3(L.v1), C = ld3(L.v2);
+        const v3 p = (C + (A - C) * (1.0f - su)) + (B - C) * (vv * su);
+        const v3 dd = p - x;
+        tmax = length(dd);
+        const float dn = dot(dd, ld3(L.Ng));
+        if (dn >= 0.0f) return mk(0, 0, 0);
+        wi = dd / tmax;
+        pdf = (2.0f * tmax * tmax * tmax) / __builtin_fabsf(dn);
+        return ld3(L.Le);
+    }
+    const v3 center = ld3(L.center);
+    const float radius = L.radius;
+    v3 dz = center - x;
+    const float dz_len_2 = dot(dz, dz);
+    const float dz_len = __builtin_sqrtf(dz_len_2);
+    dz = dz / mk(-dz_len, -dz_len, -dz_len);
+    v3 dx, dy;
+    onb(dz, dx, dy);
+    const float sin_theta_max_2 = radius * radius / dz_len_2;
+    const float sin_theta_max = __builtin_sqrtf(sin_theta_max_2);
+    const float cos_theta_max = __builtin_sqrtf(smax(0.f, 1.f - sin_theta_max_2));
+    const float cos_theta = 1.0f + (cos_theta_max - 1.0f) * rng.next();
+    const float sin_theta_2 = 1.f - cos_theta * cos_theta;
+    const float cos_alpha =
+        sin_theta_2 / sin_theta_max + cos_theta * __builtin_sqrtf(smax(0.0f, 1.0f - sin_theta_2 / sin_theta_max_2));
+    const float sin_alpha = __builtin_sqrtf(smax(0.0f, 1.0f - cos_alpha * cos_alpha));
+    const float phi = kPI_MUL_2 * rng.next();
+    const v3 nn = (dx * (glibc_cosf(phi) * sin_alpha) + dy * (glibc_sinf(phi) * sin_alpha)) + dz * cos_alpha;
+    const v3 p = center + nn * radius;
+    const v3 dd = p - x;
+    tmax = length(dd);
+    if (dot(dd, nn) >= 0.0f) return mk(0, 0, 0);
+    pdf = 1.f / (kPI_MUL_2 * (1.f - cos_theta_max));
+    wi = dd / tmax;
+    return ld3(L.Le);
+}
+
+// Lambert::sampleDir + uniformSampleHemisphere (Src/material.h:55-73)
+__device__ __forceinline__ v3 lambert_sample(const Surf& S, Rng& rng) {
+    const float r1 = rng.next();
+    const float r2 = rng.next();
+    const float sinTheta = __builtin_sqrtf(1.0f - r1 * r1);
+    const float phi = 2.0f * kPI * r2;
+    const float x = sinTheta * glibc_cosf(phi);
+    const float z = sinTheta * glibc_sinf(phi);
+    return local_to_world(mk(x, r1, z), S.dpdu, S.ng, S.dpdv);
+}
+
+__device__ __forceinline__ v3 eval_bxdf(const DObj& ob) {   // Lambert::evaluateBxDF
+    return ob.material == 1 ? ld3(ob.albedo) / kPI : mk(0, 0, 0);
+}
+
+// PinholeCamera::sampleRay (Src/camera.h:49-60)
+__device__ __forceinline__ void camera_ray(const KParams& P, float u, float v, v3& o, v3& d) {
+    const v3 dir = mk((2.0f * u - 1.0f) * P.scale, (1.0f - 2.0f * v) * P.scale / P.aspect, -1.0f);
+    const float* x = P.c2w;
+    const v3 w = mk(dir.x * x[0] + dir.y * x[4] + dir.z * x[8], dir.x * x[1] + dir.y * x[5] + dir.z * x[9],
+                    dir.x * x[2] + dir.y * x[6] + dir.z * x[10]);
+    d = normalize(w);
+    o = mk(x[12], x[13], x[14]);
+}
+
+// =================================================================== k_shade ====
+template <int SCN, int INTEG>
+__global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __restrict__ list,
+                                                   const uint32_t* __restrict__ count, uint32_t* __restrict__ out,
+                                                   uint32_t* out_count) {
+    __shared__ uint32_t lds_twist[kBlock / 64][2 * kMT];
+    const uint32_t n = *count;
+    const int tid = threadIdx.x, lane = tid & 63;
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const uint32_t i = base + tid;
+        const bool valid = i < n;
+        const uint32_t s = valid ? list[i] : 0;
+        uint32_t g = valid ? P.rng_g[s] : 0;
+        Rng rng{P.ring + (size_t)s * kRing, valid ? P.rng_c[s] : 0};
+        wave_refill(valid && (g - rng.c) < kRngMin, s, g, P.ring, lds_twist[tid >> 6], lane);
+
+        uint32_t st = valid ? P.state[s] : ST_DONE;
+        if (valid) {
+            uint32_t depth = P.depth[s];
+            uint32_t k = P.sample_k[s];
+            v3 thr = xyz(P.thr[s]), rad = xyz(P.rad[s]);
+            v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+            uint32_t nseg = 0, nsh = 0, nrej = 0;
+            bool finalize = false;
+
+            // ---- 1. resolve the previous bounce's NEE with the shadow-ray results
+            if (st & ST_NEE) {
+                const uint32_t smask = (st >> ST_SHADOW_SHIFT) & 0xffu;
+                const uint32_t occ = smask ? P.occ[s] : 0u;
+                if (INTEG == XRT_INTEGRATOR_DIRECT) {
+                    // radiance += vis * fr * L * cos / pdf per light (Src/integrator.h:95-109)
+                    for (int l = 0; l < P.n_lights; ++l) {
+                        if (!(smask & (1u << l))) continue;
+                        const v3 c = (occ & (1u << l)) ? mk(0, 0, 0) : xyz(P.sh_c[(size_t)l * P.n_slots + s]);
+                        rad = rad + c;
+                    }
+                } else {
+                    // L_light = 0 + vis*fr*L*cos/pdf; directL += L_light; radiance += thr*directL
+                    // (Src/integrator.h:249-269)
+                    v3 directL = mk(0, 0, 0);
+                    for (int l = 0; l < P.n_lights; ++l) {
+                        if (!(smask & (1u << l))) continue;
+                        const v3 c = (occ & (1u << l)) ? mk(0, 0, 0) : xyz(P.sh_c[(size_t)l * P.n_slots + s]);
+                        directL = directL + (mk(0, 0, 0) + c);
+                    }
+                    rad = rad + xyz(P.thr_prev[s]) * directL;
+                }
+                st &= ~(ST_NEE | (0xffu << ST_SHADOW_SHIFT));
+                if (st & ST_END) finalize = true;
+            }
+
+            // ---- 2. shade the traced extension ray
+            if (st & ST_RAY) {
+                st &= ~ST_RAY;
+                ++nseg;
+                o = xyz(P.ray_o[s]);
+                d = xyz(P.ray_d[s]);
+                Surf S;
+                float t1;
+                const int obj = surface<SCN>(P, s, o, d, P.hit[s], S, t1);
+                if (INTEG == XRT_INTEGRATOR_DIRECT) {
+                    // DirectIntegrator::integrate (Src/integrator.h:82-119)
+                    if (obj < 0) {
+                        rad = mk((float)0.18, (float)0.18, (float)0.18);
+                        finalize = true;
+                    } else if (P.objs[obj].light >= 0) {
+                        rad = light_Le(P.lights[P.objs[obj].light], S.ns, d);
+                        finalize = true;
+                    } else {
+                        const DObj ob = P.objs[obj];
+                        uint32_t smask = 0;
+                        for (int l = 0; l < P.n_lights; ++l) {
+                            v3 wi = mk(0, 0, 0);
+                            float tmax = 0.0f, pdf = 0.0f;
+                            const v3 L = light_sample(P.lights[l], S.pos, wi, pdf, tmax, rng);
+                            if (pdf == 0.0f) continue;
+                            const float bias = 0.01f;
+                            const float cosv = smax(0.0f, dot(S.ng, wi));
+                            const v3 fr = eval_bxdf(ob);
+                            P.sh_o[(size_t)l * P.n_slots + s] = pk(S.pos + S.ng * bias, tmax - bias);
+                            P.sh_d[(size_t)l * P.n_slots + s] = pk(wi);
+                            P.sh_c[(size_t)l * P.n_slots + s] = pk(((fr * L) * cosv) / pdf);
+                            smask |= 1u << l;
+                            ++nsh;
+                        }
+                        if (smask) st |= ST_NEE | ST_END | (smask << ST_SHADOW_SHIFT);
+                        else finalize = true;
+                    }
+                } else {
+                    // GIIntegrator::integrate loop body (Src/integrator.h:214-284)
+                    if (obj < 0) {
+                        rad = rad + thr * mk(0.0f, 0.0f, 0.0f);
+                        finalize = true;
+                    } else {
+                        bool alive = true;
+                        if (depth > 0) {
+                            const float p = smin((thr.x + thr.y + thr.z) / 3.0f, 1.0f);
+                            if (rng.next() >= p) alive = false, finalize = true;
+                            else thr = thr / mk(p, p, p);
+                        }
+                        const DObj ob = P.objs[obj];
+                        if (alive && ob.light >= 0) {
+                            if (depth == 0) rad = rad + thr * light_Le(P.lights[ob.light], S.ns, d);
+                            alive = false, finalize = true;
+                        }
+                        if (alive) {
+                            uint32_t smask = 0;
+                            for (int l = 0; l < P.n_lights; ++l) {
+                                v3 wi = mk(0, 0, 0);
+                                float tmax = 0.0f, pdf = 0.0f;
+                                const v3 L = light_sample(P.lights[l], S.pos, wi, pdf, tmax, rng);
+                                if (pdf == 0.0f) continue;
+                                const float bias = 0.01f;
+                                const float cosv = smax(0.0f, dot(S.ng, wi));
+                                const v3 fr = eval_bxdf(ob);
+                                P.sh_o[(size_t)l * P.n_slots + s] = pk(S.pos + S.ng * bias, tmax - bias);
+                                P.sh_d[(size_t)l * P.n_slots + s] = pk(wi);
+                                P.sh_c[(size_t)l * P.n_slots + s] = pk(((fr * L) * cosv) / pdf);
+                                smask |= 1u << l;
+                                ++nsh;
+                            }
+                            if (smask) {
+                                P.thr_prev[s] = pk(thr);
+                                st |= ST_NEE | (smask << ST_SHADOW_SHIFT);
+                            } else {
+                                rad = rad + thr * mk(0, 0, 0);   // radiance += thr * directL(=0)
+                            }
+                            // indirect: Object::sampleBxDF -> Lambert (no material: 0, no draws)
+                            float pdf = 1.0f;
+                            v3 nd = mk(0, 0, 0), fr = mk(0, 0, 0);
+                            if (ob.material == 1) {
+                                nd = lambert_sample(S, rng);
+                                pdf = 1.0f / (2.0f * kPI);
+                                fr = eval_bxdf(ob);
+                            }
+                            const float cosv = smax(0.0f, dot(nd, S.ng));
+                            thr = thr * ((fr * cosv) / pdf);
+                            o = S.pos + S.ng * 0.01f;
+                            d = nd;
+                            ++depth;
+                            if (depth < P.max_depth) {
+                                st |= ST_RAY;
+                                P.ray_o[s] = pk(o);
+                                P.ray_d[s] = pk(d);
+                            } else if (smask) {
+                                st |= ST_END;
+                            } else {
+                                finalize = true;
+                            }
+                        }
+                    }
+                }
+            }
+
+            // ---- 3. finish the sample, start the next one (Src/renderer.cpp:42-76)
+            while (finalize) {
+                finalize = false;
+                if (st & ST_REGEN) {
+                    st &= ~ST_REGEN;
+                } else {
+                    const v3 r = rad / 1.0f;   // integrate(...) / pdf, pdf = 1
+                    if (__builtin_isnan(r.x) || __builtin_isnan(r.y) || __builtin_isnan(r.z) ||
+                        __builtin_isinf(r.x) || __builtin_isinf(r.y) || __builtin_isinf(r.z) ||
+                        r.x < 0.0f || r.y < 0.0f || r.z < 0.0f) {
+                        ++nrej;
+                    } else {
+                        const uint32_t col = s % P.width, row = P.shard_index + P.shard_count * (s / P.width);
+                        float* px = P.fb + 3 * ((size_t)col + (size_t)P.width * row);
+                        px[0] = px[0] + r.x, px[1] = px[1] + r.y, px[2] = px[2] + r.z;
+                    }
+                    ++k;
+                }
+                st &= ~(ST_END | ST_RAY);
+                if (k >= P.spp) {
+                    st = ST_DONE;
+                    break;
+                }
+                // regenerate: jitter draws, camera ray
+                const uint32_t col = s % P.width, row = P.shard_index + P.shard_count * (s / P.width);
+                const float u = ((float)(int)col + rng.next()) / (float)P.width;
+                const float v = ((float)(int)row + rng.next()) / (float)P.height;
+                camera_ray(P, u, v, o, d);
+                thr = mk(1, 1, 1);
+                rad = mk(0, 0, 0);
+                depth = 0;
+                if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) {
+                    finalize = true;   // the bounce loop never runs: radiance 0
+                    continue;
+                }
+                st |= ST_RAY;
+                P.ray_o[s] = pk(o);
+                P.ray_d[s] = pk(d);
+            }
+            if (st & ST_REGEN) {   // very first sample of the slot
+                st &= ~ST_REGEN;
+                const uint32_t col = s % P.width, row = P.shard_index + P.shard_count * (s / P.width);
+                const float u = ((float)(int)col + rng.next()) / (float)P.width;
+                const float v = ((float)(int)row + rng.next()) / (float)P.height;
+                camera_ray(P, u, v, o, d);
+                thr = mk(1, 1, 1);
+                rad = mk(0, 0, 0);
+                depth = 0;
+                if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) {
+                    // degenerate: every sample is 0 — finish all of them here
+                    while (true) {
+                        ++k;
+                        if (k >= P.spp) { st = ST_DONE; break; }
+                        (void)rng.next(), (void)rng.next();
+                    }
+                } else {
+                    st |= ST_RAY;
+                    P.ray_o[s] = pk(o);
+                    P.ray_d[s] = pk(d);
+                }
+            }
+            P.state[s] = st;
+            P.depth[s] = depth;
+            P.sample_k[s] = k;
+            P.thr[s] = pk(thr);
+            P.rad[s] = pk(rad);
+            P.rng_c[s] = rng.c;
+            P.rng_g[s] = g;
+            if (nseg) P.c_seg[s] += nseg;
+            if (nsh) P.c_shadow[s] += nsh;
+            if (nrej) P.c_rej[s] += nrej;
+        }
+        // ---- 4. compaction: ballot + prefix count, one atomic per wave
+        const bool keep = valid && !(st & ST_DONE);
+        const uint64_t m = __ballot(keep);
+        if (m) {
+            const uint32_t cnt = __popcll(m);
+            const uint32_t pre = __popcll(m & ((1ull << lane) - 1ull));
+            uint32_t wbase = 0;
+            if (lane == __ffsll((unsigned long long)m) - 1) wbase = atomicAdd(out_count, cnt);
+            wbase = __shfl(wbase, __ffsll((unsigned long long)m) - 1);
+            if (keep) out[wbase + pre] = s;
+        }
+    }
+}
+
+// ================================================================== k_finish ====
+// Image::operator/=(Vec3f(n_samples)) over this shard's pixels + counter reduction.
+__global__ __launch_bounds__(kBlock) void k_finish(KParams P) {
+    __shared__ unsigned long long red[5][kBlock / 64];
+    unsigned long long a[5] = {0, 0, 0, 0, 0};
+    const float n = (float)P.spp;
+    for (uint32_t s = blockIdx.x * kBlock + threadIdx.x; s < P.n_slots; s += gridDim.x * kBlock) {
+        const uint32_t col = s % P.width, row = P.shard_index + P.shard_count * (s / P.width);
+        float* px = P.fb + 3 * ((size_t)col + (size_t)P.width * row);
+        px[0] = px[0] / n, px[1] = px[1] / n, px[2] = px[2] / n;
+        a[0] += P.c_seg[s];
+        a[1] += P.c_shadow[s];
+        a[2] += P.rng_c[s] - kMT;
+        a[3] += P.c_rej[s];
+        a[4] += P.c_stall[s];
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        unsigned long long v = a[q];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
+        if (lane == 0) red[q][wv] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 5) {
+        unsigned long long v = 0;
+        for (int w = 0; w < kBlock / 64; ++w) v += red[threadIdx.x][w];
+        atomicAdd(P.stats + threadIdx.x, v);
+    }
+}
+
+// ============================================================== self-tests ====
+__global__ __launch_bounds__(kBlock) void k_test_rng(const uint32_t* seeds, uint32_t n_seeds, uint32_t skip,
+                                                      uint32_t n, float* out, uint32_t* rings) {
+    __shared__ uint32_t lds_twist[kBlock / 64][2 * kMT];
+    const int lane = threadIdx.x & 63;
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    const bool valid = s < n_seeds;
+    uint32_t* ring = rings + (size_t)s * kRing;
+    if (valid) {
+        uint32_t x = seeds[s];
+        ring[0] = x;
+        for (uint32_t i = 1; i < kMT; ++i) {
+            x = 1812433253u * (x ^ (x >> 30)) + i;
+            ring[i] = x;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    uint32_t g = kMT;
+    Rng rng{ring, kMT};
+    // consume skip + n draws, refilling cooperatively like k_shade does
+    const uint32_t total = skip + n;
+    for (uint32_t done = 0; done < total;) {
+        wave_refill(valid && (g - rng.c) < kRngMin, s, g, rings, lds_twist[threadIdx.x >> 6], lane);
+        const uint32_t chunk = min(32u, total - done);   // < kRngMin: never reads past g
+        if (valid) {
+            for (uint32_t q = 0; q < chunk; ++q) {
+                const uint32_t idx = done + q;
+                const float f = rng.next();
+                if (idx >= skip) out[(size_t)s * n + (idx - skip)] = f;
+            }
+        }
+        done += chunk;
+    }
+}
+
+__global__ void k_test_trig(const float* x, uint32_t n, float* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        out[2 * i] = glibc_sinf(x[i]);
+        out[2 * i + 1] = glibc_cosf(x[i]);
+    }
+}
+
+// every float r in [0,1) with bit pattern in [first, first+count) that the sampler can
+// produce (r * 2^32 integral): phi = 2*PI*r -> (sin, cos); others -> NaN marker in out_r
+__global__ void k_test_trig_domain(uint32_t first, uint32_t count, float* out_sin, float* out_cos, float* out_r) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const float r = __uint_as_float(first + i);
+    const double sc = (double)r * 4294967296.0;
+    const bool reach = r >= 0.0f && r < 1.0f && sc == __builtin_floor(sc);
+    const float phi = kPI_MUL_2 * r;
+    out_r[i] = reach ? r : __builtin_nanf("");
+    out_sin[i] = glibc_sinf(phi);
+    out_cos[i] = glibc_cosf(phi);
+}
+
+// ================================================================== launchers ====
+}  // namespace xrt
+
+#include "launch.h"
+
+namespace xrt {
+
+hipError_t launch_seed(const KParams& P, uint32_t* list, uint32_t* count, uint32_t* count_other, hipStream_t st) {
+    const uint32_t blocks = (P.n_slots + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_seed, dim3(blocks), dim3(kBlock), 0, st, P, list, count, count_other);
+    return hipGetLastError();
+}
+
+template <int SCN>
+static hipError_t trace_nl(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
+                           uint32_t blocks, hipStream_t st) {
+    if (P.n_lights <= 1)
+        hipLaunchKernelGGL((k_trace<SCN, 1>), dim3(blocks), dim3(kBlock), 0, st, P, list, count, zero);
+    else
+        hipLaunchKernelGGL((k_trace<SCN, kMaxLights>), dim3(blocks), dim3(kBlock), 0, st, P, list, count, zero);
+    return hipGetLastError();
+}
+
+hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
+                        uint32_t blocks, hipStream_t st) {
+    switch (P.scene_kind) {
+        case SCN_TRI: return trace_nl<SCN_TRI>(P, list, count, zero, blocks, st);
+        case SCN_SPHERE: return trace_nl<SCN_SPHERE>(P, list, count, zero, blocks, st);
+        default: return trace_nl<SCN_MIXED>(P, list, count, zero, blocks, st);
+    }
+}
+
+template <int SCN>
+static hipError_t shade_i(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
+                          uint32_t* out_count, uint32_t blocks, hipStream_t st) {
+    if (P.integrator == XRT_INTEGRATOR_DIRECT)
+        hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_DIRECT>), dim3(blocks), dim3(kBlock), 0, st, P, list,
+                           count, out, out_count);
+    else
+        hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_GI>), dim3(blocks), dim3(kBlock), 0, st, P, list, count,
+                           out, out_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_shade(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
+                        uint32_t* out_count, uint32_t blocks, hipStream_t st) {
+    switch (P.scene_kind) {
+        case SCN_TRI: return shade_i<SCN_TRI>(P, list, count, out, out_count, blocks, st);
+        case SCN_SPHERE: return shade_i<SCN_SPHERE>(P, list, count, out, out_count, blocks, st);
+        default: return shade_i<SCN_MIXED>(P, list, count, out, out_count, blocks, st);
+    }
+}
+
+hipError_t launch_finish(const KParams& P, hipStream_t st) {
+    const uint32_t blocks = std::min<uint32_t>((P.n_slots + kBlock - 1) / kBlock, 2048u);
+    hipLaunchKernelGGL(k_finish, dim3(blocks), dim3(kBlock), 0, st, P);
+    return hipGetLastError();
+}
+
+hipError_t launch_test_rng(const uint32_t* seeds, uint32_t n_seeds, uint32_t skip, uint32_t n, float* out,
+                           uint32_t* rings, hipStream_t st) {
+    const uint32_t blocks = (n_seeds + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_test_rng, dim3(blocks), dim3(kBlock), 0, st, seeds, n_seeds, skip, n, out, rings);
+    return hipGetLastError();
+}
+
+hipError_t launch_test_trig(const float* x, uint32_t n, float* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_test_trig, dim3((n + 255) / 256), dim3(256), 0, st, x, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_test_trig_domain(uint32_t first, uint32_t count, float* s, float* c, float* r, hipStream_t st) {
+    hipLaunchKernelGGL(k_test_trig_domain, dim3((count + 255) / 256), dim3(256), 0, st, first, count, s, c, r);
+    return hipGetLastError();
+}
+
+}  // namespace xrt

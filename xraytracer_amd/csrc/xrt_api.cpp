@@ -1,0 +1,496 @@
+// xrt_api.cpp — the C ABI of include/xrt.h: device context, scene upload, and the
+// wavefront pass schedule that replaces NormalRenderer::render / ParallelRenderer::render
+// (Src/renderer.cpp:8-27, 83-99).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "launch.h"
+#include "wavefront.h"
+#include "xrt.h"
+#include "xrt/geometry.h"
+
+using namespace xrt;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct xrt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // scene
+    std::vector<DevBuf*> scene_bufs;
+    DevBuf tri, tri_ng, tri_nrm, sph, sph_obj, box, objs, lights, segs, density;
+    KParams base{};
+    bool has_scene = false, has_camera = false, has_medium = false;
+    // slots
+    size_t cap_slots = 0;
+    DevBuf ray_o, ray_d, thr, rad, thr_prev, hit, hit2, hit3, sh_o, sh_d, sh_c, med, med2;
+    DevBuf state, sample_k, depth, occ, rng_c, rng_g, ring, c_seg, c_shadow, c_rej, c_stall, lists;
+    DevBuf counts, stats, fb, scratch;
+    size_t cap_fb = 0;
+    uint32_t* h_poll = nullptr;  // pinned
+    std::vector<hipEvent_t> events;
+};
+
+namespace {
+
+int set_err(xrt_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+int hip_err(xrt_ctx* c, hipError_t e, const char* what) {
+    return set_err(c, XRT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(ctx, expr)                                    \
+    do {                                                     \
+        hipError_t e_ = (expr);                              \
+        if (e_ != hipSuccess) return hip_err(ctx, e_, #expr); \
+    } while (0)
+
+void free_buf(DevBuf& b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+int ensure(xrt_ctx* c, DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return XRT_OK;
+    free_buf(b);
+    if (bytes == 0) return XRT_OK;
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess) {
+        b.p = nullptr;
+        return set_err(c, XRT_ERR_OOM, std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e));
+    }
+    b.bytes = bytes;
+    return XRT_OK;
+}
+
+int upload(xrt_ctx* c, DevBuf& b, const void* src, size_t bytes) {
+    int rc = ensure(c, b, std::max<size_t>(bytes, 16));
+    if (rc) return rc;
+    if (bytes) HIPCHK(c, hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+    return XRT_OK;
+}
+
+template <typename T>
+T* as(DevBuf& b) {
+    return reinterpret_cast<T*>(b.p);
+}
+
+uint32_t shard_rows(uint32_t h, uint32_t idx, uint32_t n) { return idx < h ? (h - idx + n - 1) / n : 0; }
+
+}  // namespace
+
+extern "C" {
+
+int xrt_abi_version(void) { return XRT_ABI_VERSION; }
+
+int xrt_create(int device, xrt_ctx** out) {
+    if (!out) return XRT_ERR_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return XRT_ERR_HIP;
+    if (device < 0 || device >= n) return XRT_ERR_INVALID;
+    xrt_ctx* c = new xrt_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_poll, 64 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+        delete c;
+        return XRT_ERR_HIP;
+    }
+    *out = c;
+    return XRT_OK;
+}
+
+void xrt_destroy(xrt_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    DevBuf* all[] = {&c->tri, &c->tri_ng, &c->tri_nrm, &c->sph, &c->sph_obj, &c->box, &c->objs, &c->lights,
+                     &c->segs, &c->density, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
+                     &c->hit2, &c->hit3, &c->sh_o, &c->sh_d, &c->sh_c, &c->med, &c->med2, &c->state,
+                     &c->sample_k, &c->depth, &c->occ, &c->rng_c, &c->rng_g, &c->ring, &c->c_seg, &c->c_shadow,
+                     &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch};
+    for (DevBuf* b : all) free_buf(*b);
+    for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
+    if (c->h_poll) (void)hipHostFree(c->h_poll);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* xrt_last_error(const xrt_ctx* c) { return c ? c->err.c_str() : "no context (xrt_create failed: no HIP device?)"; }
+
+// Flattened Scene -> device layout.  Primitives are re-packed in object iteration order,
+// so the linear scan order equals Scene::intersect's order (Src/scene.cpp:190-200).
+int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
+    if (!c || !s) return XRT_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (s->n_lights > (uint32_t)kMaxLights)
+        return set_err(c, XRT_ERR_UNSUPPORTED, "more than " + std::to_string(kMaxLights) + " area lights");
+    if ((s->n_objects && !s->objects) || (s->n_lights && !s->lights))
+        return set_err(c, XRT_ERR_INVALID, "null scene arrays");
+    std::vector<f4> tri, tri_ng, tri_nrm, sph, box;
+    std::vector<int> sph_obj;
+    std::vector<DObj> objs;
+    std::vector<DSeg> segs;
+    auto V = [](const float* p) { return Vec3f(p[0], p[1], p[2]); };
+    auto F4 = [](const Vec3f& v, float w) { return f4{v[0], v[1], v[2], w}; };
+    auto bits = [](int x) { float f; std::memcpy(&f, &x, 4); return f; };
+    for (uint32_t k = 0; k < s->n_objects; ++k) {
+        const xrt_object& o = s->objects[k];
+        if (o.light >= (int)s->n_lights || o.count < 0 || o.first < 0)
+            return set_err(c, XRT_ERR_INVALID, "object " + std::to_string(k) + ": bad light index or range");
+        DObj d{};
+        d.kind = o.kind, d.material = o.material, d.light = o.light, d.medium = o.medium;
+        for (int q = 0; q < 3; ++q) d.albedo[q] = o.albedo[q];
+        objs.push_back(d);
+        const bool occluder = o.light < 0;  // Scene::occluded skips area-light objects
+        int kind = -1, first = 0;
+        if (o.kind == XRT_OBJ_MESH) {
+            if ((uint64_t)o.first + o.count > s->n_tris || (o.count && (!s->tri_v || !s->tri_n)))
+                return set_err(c, XRT_ERR_INVALID, "mesh range out of bounds");
+            kind = SEG_TRI;
+            first = (int)(tri.size() / 3);
+            for (int t = o.first; t < o.first + o.count; ++t) {
+                const float* v = s->tri_v + 9 * (size_t)t;
+                const float* n = s->tri_n + 9 * (size_t)t;
+                const Vec3f v0 = V(v), v1 = V(v + 3), v2 = V(v + 6);
+                const Vec3f e1 = v1 - v0, e2 = v2 - v0;     // Src/primitive.cpp:142-143
+                tri.push_back(F4(v0, bits((int)k)));
+                tri.push_back(F4(e1, occluder ? 1.0f : 0.0f));
+                tri.push_back(F4(e2, 0.0f));
+                tri_ng.push_back(F4(normalize(cross(e1, e2)), 0.0f));   // Src/primitive.cpp:106
+                tri_nrm.push_back(F4(V(n), 0.0f));
+                tri_nrm.push_back(F4(V(n + 3), 0.0f));
+                tri_nrm.push_back(F4(V(n + 6), 0.0f));
+            }
+        } else if (o.kind == XRT_OBJ_SPHERE) {
+            if ((uint64_t)o.first + o.count > s->n_spheres || !s->spheres)
+                return set_err(c, XRT_ERR_INVALID, "sphere range out of bounds");
+            kind = SEG_SPHERE;
+            first = (int)sph.size();
+            for (int t = o.first; t < o.first + o.count; ++t) {
+                const float* p = s->spheres + 4 * (size_t)t;
+                sph.push_back(f4{p[0], p[1], p[2], p[3]});
+                sph_obj.push_back((int)k | (occluder ? (1 << 30) : 0));
+            }
+        } else if (o.kind == XRT_OBJ_BOX) {
+            if ((uint64_t)o.first + o.count > s->n_boxes || !s->boxes)
+                return set_err(c, XRT_ERR_INVALID, "box range out of bounds");
+            kind = SEG_BOX;
+            first = (int)(box.size() / 2);
+            for (int t = o.first; t < o.first + o.count; ++t) {
+                const float* p = s->boxes + 6 * (size_t)t;
+                box.push_back(f4{p[0], p[1], p[2], bits((int)k)});
+                box.push_back(f4{p[3], p[4], p[5], 0.0f});
+            }
+        } else {
+            return set_err(c, XRT_ERR_INVALID, "unknown object kind");
+        }
+        if (o.count == 0) continue;
+        if (!segs.empty() && segs.back().kind == kind && segs.back().first + segs.back().count == first)
+            segs.back().count += o.count;
+        else
+            segs.push_back(DSeg{kind, first, o.count, 0});
+    }
+    std::vector<DLight> lights;
+    for (uint32_t l = 0; l < s->n_lights; ++l) {
+        const xrt_light& L = s->lights[l];
+        DLight d{};
+        d.kind = L.kind;
+        const Vec3f v0 = V(L.v0), v1 = V(L.v1), v2 = V(L.v2);
+        const Vec3f e1 = v1 - v0, e2 = v2 - v0, Ng = cross(e1, e2);   // QuadLight/TriangleLight ctor
+        for (int q = 0; q < 3; ++q) {
+            d.v0[q] = v0[q], d.v1[q] = v1[q], d.v2[q] = v2[q];
+            d.e1[q] = e1[q], d.e2[q] = e2[q], d.Ng[q] = Ng[q];
+            d.center[q] = L.center[q], d.Le[q] = L.Le[q];
+        }
+        d.radius = L.radius;
+        lights.push_back(d);
+    }
+    int rc;
+    if ((rc = upload(c, c->tri, tri.data(), tri.size() * sizeof(f4))) ||
+        (rc = upload(c, c->tri_ng, tri_ng.data(), tri_ng.size() * sizeof(f4))) ||
+        (rc = upload(c, c->tri_nrm, tri_nrm.data(), tri_nrm.size() * sizeof(f4))) ||
+        (rc = upload(c, c->sph, sph.data(), sph.size() * sizeof(f4))) ||
+        (rc = upload(c, c->sph_obj, sph_obj.data(), sph_obj.size() * sizeof(int))) ||
+        (rc = upload(c, c->box, box.data(), box.size() * sizeof(f4))) ||
+        (rc = upload(c, c->objs, objs.data(), objs.size() * sizeof(DObj))) ||
+        (rc = upload(c, c->lights, lights.data(), lights.size() * sizeof(DLight))) ||
+        (rc = upload(c, c->segs, segs.data(), segs.size() * sizeof(DSeg))))
+        return rc;
+    KParams& P = c->base;
+    P.tri = as<f4>(c->tri), P.tri_ng = as<f4>(c->tri_ng), P.tri_nrm = as<f4>(c->tri_nrm);
+    P.sph = as<f4>(c->sph), P.sph_obj = as<int>(c->sph_obj), P.box = as<f4>(c->box);
+    P.objs = as<DObj>(c->objs), P.lights = as<DLight>(c->lights), P.segs = as<DSeg>(c->segs);
+    P.n_segs = (int)segs.size(), P.n_lights = (int)lights.size();
+    P.n_tris = (int)(tri.size() / 3), P.n_sph = (int)sph.size(), P.n_box = (int)(box.size() / 2);
+    bool only_tri = true, only_sph = true;
+    for (const DSeg& g : segs) only_tri &= g.kind == SEG_TRI, only_sph &= g.kind == SEG_SPHERE;
+    P.scene_kind = (only_tri || segs.empty()) ? SCN_TRI : (only_sph ? SCN_SPHERE : SCN_MIXED);
+    c->has_scene = true;
+    return XRT_OK;
+}
+
+int xrt_set_camera(xrt_ctx* c, const float c2w[16], float scale, float aspect) {
+    if (!c || !c2w) return XRT_ERR_INVALID;
+    std::memcpy(c->base.c2w, c2w, sizeof(float) * 16);
+    c->base.scale = scale;
+    c->base.aspect = aspect;
+    c->has_camera = true;
+    return XRT_OK;
+}
+
+int xrt_set_medium(xrt_ctx* c, const xrt_medium_desc* m) {
+    if (!c || !m || !m->density || !m->nx || !m->ny || !m->nz) return XRT_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t n = (size_t)m->nx * m->ny * m->nz;
+    int rc = upload(c, c->density, m->density, n * sizeof(float));
+    if (rc) return rc;
+    DMedium& D = c->base.medium;
+    D.density = as<float>(c->density);
+    D.nx = (int)m->nx, D.ny = (int)m->ny, D.nz = (int)m->nz;
+    for (int q = 0; q < 3; ++q) {
+        D.origin[q] = m->origin[q];
+        D.absorption[q] = m->absorption[q];
+        D.scattering[q] = m->scattering[q];
+    }
+    D.voxel_size = m->voxel_size;
+    D.multiplier = m->density_multiplier;
+    D.g = m->g;
+    // HeterogeneousMedium ctor (Src/medium.cpp:5-17)
+    const float max_density = m->density_multiplier * m->max_density;
+    const Vec3f a(m->absorption[0], m->absorption[1], m->absorption[2]);
+    const Vec3f sc(m->scattering[0], m->scattering[1], m->scattering[2]);
+    const Vec3f mm = a * max_density + sc * max_density;
+    D.majorant = std::max(mm[0], std::max(mm[1], mm[2]));
+    D.inv_majorant = 1.0f / D.majorant;
+    c->has_medium = true;
+    return XRT_OK;
+}
+
+static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, float* h_out, xrt_stats* st) {
+    const auto t_start = std::chrono::steady_clock::now();
+    if (!c || !p) return XRT_ERR_INVALID;
+    if (!c->has_scene || !c->has_camera) return set_err(c, XRT_ERR_STATE, "upload a scene and set a camera first");
+    if (p->width == 0 || p->height == 0 || p->shard_count == 0 || p->shard_index >= p->shard_count)
+        return set_err(c, XRT_ERR_INVALID, "bad image size or shard");
+    if (p->integrator != XRT_INTEGRATOR_GI && p->integrator != XRT_INTEGRATOR_DIRECT)
+        return set_err(c, XRT_ERR_UNSUPPORTED, "integrator not implemented");
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint32_t rows = shard_rows(p->height, p->shard_index, p->shard_count);
+    const size_t n = (size_t)rows * p->width;
+    const size_t npix = (size_t)p->width * p->height;
+    int rc;
+    if (n > c->cap_slots) {
+        const size_t L = kMaxLights;
+        if ((rc = ensure(c, c->ray_o, n * 16)) || (rc = ensure(c, c->ray_d, n * 16)) || (rc = ensure(c, c->thr, n * 16)) ||
+            (rc = ensure(c, c->rad, n * 16)) || (rc = ensure(c, c->thr_prev, n * 16)) || (rc = ensure(c, c->hit, n * 16)) ||
+            (rc = ensure(c, c->hit2, n * 16)) || (rc = ensure(c, c->hit3, n * 16)) ||
+            (rc = ensure(c, c->sh_o, L * n * 16)) || (rc = ensure(c, c->sh_d, L * n * 16)) ||
+            (rc = ensure(c, c->sh_c, L * n * 16)) || (rc = ensure(c, c->med, n * 16)) || (rc = ensure(c, c->med2, n * 16)) ||
+            (rc = ensure(c, c->state, n * 4)) || (rc = ensure(c, c->sample_k, n * 4)) || (rc = ensure(c, c->depth, n * 4)) ||
+            (rc = ensure(c, c->occ, n * 4)) || (rc = ensure(c, c->rng_c, n * 4)) || (rc = ensure(c, c->rng_g, n * 4)) ||
+            (rc = ensure(c, c->ring, n * kRing * 4)) || (rc = ensure(c, c->c_seg, n * 4)) ||
+            (rc = ensure(c, c->c_shadow, n * 4)) || (rc = ensure(c, c->c_rej, n * 4)) || (rc = ensure(c, c->c_stall, n * 4)) ||
+            (rc = ensure(c, c->lists, 2 * n * 4)))
+            return rc;
+        c->cap_slots = n;
+    }
+    if ((rc = ensure(c, c->counts, 64)) || (rc = ensure(c, c->stats, 64))) return rc;
+    float* fb = d_out;
+    if (!fb) {
+        if ((rc = ensure(c, c->fb, npix * 3 * sizeof(float)))) return rc;
+        fb = as<float>(c->fb);
+    }
+    KParams P = c->base;
+    P.integrator = p->integrator;
+    P.max_depth = p->max_depth, P.width = p->width, P.height = p->height, P.spp = p->spp;
+    P.shard_index = p->shard_index, P.shard_count = p->shard_count, P.n_slots = (uint32_t)n;
+    P.ray_o = as<f4>(c->ray_o), P.ray_d = as<f4>(c->ray_d), P.thr = as<f4>(c->thr), P.rad = as<f4>(c->rad);
+    P.thr_prev = as<f4>(c->thr_prev), P.hit = as<f4>(c->hit), P.hit2 = as<f4>(c->hit2), P.hit3 = as<f4>(c->hit3);
+    P.sh_o = as<f4>(c->sh_o), P.sh_d = as<f4>(c->sh_d), P.sh_c = as<f4>(c->sh_c);
+    P.med = as<f4>(c->med), P.med2 = as<f4>(c->med2);
+    P.state = as<uint32_t>(c->state), P.sample_k = as<uint32_t>(c->sample_k), P.depth = as<uint32_t>(c->depth);
+    P.occ = as<uint32_t>(c->occ), P.rng_c = as<uint32_t>(c->rng_c), P.rng_g = as<uint32_t>(c->rng_g);
+    P.ring = as<uint32_t>(c->ring);
+    P.c_seg = as<uint32_t>(c->c_seg), P.c_shadow = as<uint32_t>(c->c_shadow), P.c_rej = as<uint32_t>(c->c_rej);
+    P.c_stall = as<uint32_t>(c->c_stall);
+    P.fb = fb;
+    P.stats = as<unsigned long long>(c->stats);
+
+    uint32_t* lists[2] = {as<uint32_t>(c->lists), as<uint32_t>(c->lists) + n};
+    uint32_t* counts = as<uint32_t>(c->counts);
+    const bool timing = (p->flags & XRT_FLAG_TIMING) != 0;
+    xrt_stats S;
+    std::memset(&S, 0, sizeof(S));
+    S.path_slots = n;
+    S.samples = (uint64_t)n * p->spp;
+    std::vector<std::pair<int, size_t>> ev_use;   // (kernel id, first event index)
+    size_t ev_next = 0;
+    auto ev_pair = [&](int kid) -> size_t {
+        while (c->events.size() < ev_next + 2) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return (size_t)-1;
+            c->events.push_back(e);
+        }
+        const size_t i = ev_next;
+        ev_next += 2;
+        ev_use.push_back({kid, i});
+        return i;
+    };
+    auto launch = [&](int kid, auto&& fn) -> hipError_t {
+        size_t e = timing ? ev_pair(kid) : (size_t)-1;
+        if (e != (size_t)-1) (void)hipEventRecord(c->events[e], c->stream);
+        hipError_t err = fn();
+        if (e != (size_t)-1) (void)hipEventRecord(c->events[e + 1], c->stream);
+        S.launches[kid]++;
+        return err;
+    };
+
+    HIPCHK(c, hipMemsetAsync(fb, 0, npix * 3 * sizeof(float), c->stream));
+    HIPCHK(c, hipMemsetAsync(P.stats, 0, 64, c->stream));
+    HIPCHK(c, launch(XRT_K_SEED, [&] { return launch_seed(P, lists[0], counts + 0, counts + 1, c->stream); }));
+
+    const uint32_t blocks = (uint32_t)std::min<size_t>((n + 255) / 256, 8192);
+    const uint64_t cap_iters = (uint64_t)p->spp * (p->max_depth + 2) + 16;
+    // asynchronous termination polling: every kPoll iterations copy the live-slot count to
+    // pinned memory; block on a poll only when the host runs kAhead iterations ahead.
+    constexpr uint64_t kPoll = 16, kAhead = 64;
+    struct Poll { uint64_t it; hipEvent_t ev; int slot; };
+    std::vector<Poll> polls;
+    std::vector<hipEvent_t> poll_ev;
+    for (int q = 0; q < 8; ++q) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        poll_ev.push_back(e);
+    }
+    uint64_t it = 0;
+    int poll_slot = 0;
+    bool done = false;
+    for (; it < cap_iters && !done; ++it) {
+        const int cur = (int)(it & 1), nxt = cur ^ 1;
+        hipError_t e = launch(XRT_K_SHADE, [&] {
+            return launch_shade(P, lists[cur], counts + cur, lists[nxt], counts + nxt, blocks, c->stream);
+        });
+        if (e != hipSuccess) return hip_err(c, e, "k_shade");
+        if (it % kPoll == kPoll - 1) {
+            const int ps = poll_slot++ % 8;
+            HIPCHK(c, hipMemcpyAsync(c->h_poll + ps, counts + nxt, 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipEventRecord(poll_ev[ps], c->stream));
+            polls.push_back({it, poll_ev[ps], ps});
+        }
+        e = launch(XRT_K_TRACE, [&] { return launch_trace(P, lists[nxt], counts + nxt, counts + cur, blocks, c->stream); });
+        if (e != hipSuccess) return hip_err(c, e, "k_trace");
+        // retire polls: non-blocking when possible, blocking when too far ahead
+        while (!polls.empty()) {
+            Poll& q = polls.front();
+            const bool must_wait = it - q.it >= kAhead;
+            if (!must_wait && hipEventQuery(q.ev) != hipSuccess) break;
+            HIPCHK(c, hipEventSynchronize(q.ev));
+            if (c->h_poll[q.slot] == 0) done = true;
+            polls.erase(polls.begin());
+            if (done) break;
+        }
+    }
+    S.iterations = it;
+    HIPCHK(c, launch(XRT_K_FINISH, [&] { return launch_finish(P, c->stream); }));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (hipEvent_t e : poll_ev) (void)hipEventDestroy(e);
+    if (!done) {
+        // the iteration cap was reached without observing an empty list: verify
+        uint32_t left = 0;
+        HIPCHK(c, hipMemcpy(&left, counts + (it & 1), 4, hipMemcpyDeviceToHost));
+        if (left != 0) return set_err(c, XRT_ERR_HIP, "iteration cap reached with live paths");
+    }
+    unsigned long long hs[8] = {0};
+    HIPCHK(c, hipMemcpy(hs, P.stats, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    S.segments = hs[0], S.shadow_rays = hs[1], S.draws = hs[2], S.rejected = hs[3], S.stalled = hs[4];
+    if (timing) {
+        for (auto& u : ev_use) {
+            float ms = 0.0f;
+            if (hipEventElapsedTime(&ms, c->events[u.second], c->events[u.second + 1]) == hipSuccess)
+                S.kernel_ms[u.first] += ms;
+        }
+    }
+    if (h_out) HIPCHK(c, hipMemcpy(h_out, fb, npix * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    S.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    if (st) *st = S;
+    return XRT_OK;
+}
+
+int xrt_render(xrt_ctx* c, const xrt_render_params* p, float* rgb_out, xrt_stats* st) {
+    if (!rgb_out) return set_err(c, XRT_ERR_INVALID, "null output");
+    return render_impl(c, p, nullptr, rgb_out, st);
+}
+
+int xrt_render_device(xrt_ctx* c, const xrt_render_params* p, float* d_rgb_out, xrt_stats* st) {
+    if (!d_rgb_out) return set_err(c, XRT_ERR_INVALID, "null output");
+    return render_impl(c, p, d_rgb_out, nullptr, st);
+}
+
+// ---------------------------------------------------------------- self-tests ----
+int xrt_test_rng(xrt_ctx* c, const uint32_t* seeds, uint32_t n_seeds, uint32_t skip, uint32_t n, float* out) {
+    if (!c || !seeds || !out) return XRT_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    DevBuf ds, dout, rings;
+    int rc;
+    if ((rc = ensure(c, ds, n_seeds * 4)) || (rc = ensure(c, dout, (size_t)n_seeds * n * 4)) ||
+        (rc = ensure(c, rings, (size_t)n_seeds * kRing * 4)))
+        return rc;
+    hipError_t e = hipMemcpy(ds.p, seeds, n_seeds * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_test_rng(as<uint32_t>(ds), n_seeds, skip, n, as<float>(dout), as<uint32_t>(rings), c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, dout.p, (size_t)n_seeds * n * 4, hipMemcpyDeviceToHost);
+    free_buf(ds), free_buf(dout), free_buf(rings);
+    return e == hipSuccess ? XRT_OK : hip_err(c, e, "xrt_test_rng");
+}
+
+int xrt_test_trig(xrt_ctx* c, const float* x, uint32_t n, float* out) {
+    if (!c || !x || !out) return XRT_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    DevBuf dx, dout;
+    int rc;
+    if ((rc = ensure(c, dx, (size_t)n * 4 + 16)) || (rc = ensure(c, dout, (size_t)n * 8 + 16))) return rc;
+    hipError_t e = hipMemcpy(dx.p, x, (size_t)n * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_test_trig(as<float>(dx), n, as<float>(dout), c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, dout.p, (size_t)n * 8, hipMemcpyDeviceToHost);
+    free_buf(dx), free_buf(dout);
+    return e == hipSuccess ? XRT_OK : hip_err(c, e, "xrt_test_trig");
+}
+
+int xrt_test_trig_draw_domain(xrt_ctx* c, uint32_t first, uint32_t count, float* out_sin, float* out_cos, float* out_r) {
+    if (!c || !out_sin || !out_cos || !out_r) return XRT_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    DevBuf ds, dc, dr;
+    int rc;
+    const size_t b = (size_t)count * 4 + 16;
+    if ((rc = ensure(c, ds, b)) || (rc = ensure(c, dc, b)) || (rc = ensure(c, dr, b))) return rc;
+    hipError_t e = launch_test_trig_domain(first, count, as<float>(ds), as<float>(dc), as<float>(dr), c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(out_sin, ds.p, (size_t)count * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out_cos, dc.p, (size_t)count * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out_r, dr.p, (size_t)count * 4, hipMemcpyDeviceToHost);
+    free_buf(ds), free_buf(dc), free_buf(dr);
+    return e == hipSuccess ? XRT_OK : hip_err(c, e, "xrt_test_trig_draw_domain");
+}
+
+}  // extern "C"
