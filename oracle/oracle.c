@@ -840,3 +840,11 @@ void orc_kat_light(orc_mt* m, const xrt_light* l, const float* pos, float* out) 
     out[4] = tmax;
     st3(out + 5, L);
 }
+
+/* host glibc sinf/cosf over an array (the checker for the device restatement) */
+void orc_libm_sincosf(const float* x, uint32_t n, float* s, float* c) {
+    for (uint32_t i = 0; i < n; ++i) {
+        s[i] = sinf(x[i]);
+        c[i] = cosf(x[i]);
+    }
+}

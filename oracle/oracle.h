@@ -85,6 +85,9 @@ uint32_t orc_kat_wavelength(orc_mt* m, const float* thr, const float* albedo, fl
  * SphereLight::sample default branch (light.h:157-197).  out: wi[3], pdf, tmax, L[3] */
 void orc_kat_light(orc_mt* m, const xrt_light* l, const float* pos, float* out);
 
+/* host libm sinf/cosf (checker for the device restatement) */
+void orc_libm_sincosf(const float* x, uint32_t n, float* s, float* c);
+
 #ifdef __cplusplus
 }
 #endif

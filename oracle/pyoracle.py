@@ -70,6 +70,7 @@ def lib():
         l.orc_kat_wavelength.argtypes = [C.POINTER(OrcMT), f32p, f32p, f32p]
         l.orc_kat_wavelength.restype = C.c_uint32
         l.orc_kat_light.argtypes = [C.POINTER(OrcMT), C.POINTER(abi.XrtLight), f32p, f32p]
+        l.orc_libm_sincosf.argtypes = [f32p, C.c_uint32, f32p, f32p]
         _lib = l
     return _lib
 
@@ -139,3 +140,11 @@ def mt(seed) -> OrcMT:
     m = OrcMT()
     lib().orc_mt_seed(C.byref(m), seed)
     return m
+
+
+def libm_sincosf(x):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    s = np.empty_like(x)
+    c = np.empty_like(x)
+    lib().orc_libm_sincosf(fp(x), len(x), fp(s), fp(c))
+    return s, c

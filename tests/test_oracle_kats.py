@@ -1,0 +1,146 @@
+"""Oracle pinning: the C restatement (oracle/oracle.c) against known answers produced by
+the REFERENCE's own code (tests/golden/ref_kats.json, made by oracle/gen_ref_goldens.py
+from /root/reference/Src compiled in place).  Bit-exact comparisons on float bit patterns.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import pyoracle
+
+
+def f32(words):
+    return np.asarray(words, dtype=np.uint32).view(np.float32)
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def test_mt19937_uniform_streams(golden):
+    seeds = golden["rng_seeds"]
+    ref = np.asarray(golden["rng_draws_2000"], dtype=np.uint32).reshape(len(seeds), 2000)
+    for i, s in enumerate(seeds):
+        got = bits(pyoracle.draws(s, 2000))
+        assert np.array_equal(got, ref[i]), f"seed {s}: first mismatch at {np.argmax(got != ref[i])}"
+
+
+def test_mt19937_deep_stream(golden):
+    got = bits(pyoracle.draws(7, 100, skip=100000))
+    assert np.array_equal(got, np.asarray(golden["rng_seed7_skip100000"], dtype=np.uint32))
+
+
+def test_getnext2d_order(golden):
+    # Vec2f(dis(gen), dis(gen)) under GCC = (second draw, first draw) (Src/sampler.h:49)
+    ref = np.asarray(golden["rng_seed12345_next2d"], dtype=np.uint32).reshape(-1, 2)
+    d = bits(pyoracle.draws(12345, 128)).reshape(-1, 2)
+    assert np.array_equal(ref[:, 0], d[:, 1]) and np.array_equal(ref[:, 1], d[:, 0])
+
+
+def test_normalize_and_onb(golden):
+    lib = pyoracle.lib()
+    vin = f32(golden["onb_in"]).reshape(-1, 3)
+    n_ref = np.asarray(golden["onb_normalized"], np.uint32).reshape(-1, 3)
+    t_ref = np.asarray(golden["onb_t"], np.uint32).reshape(-1, 3)
+    b_ref = np.asarray(golden["onb_b"], np.uint32).reshape(-1, 3)
+    for k in range(len(vin)):
+        v = np.ascontiguousarray(vin[k])
+        n = np.zeros(3, np.float32)
+        lib.orc_kat_normalize(pyoracle.fp(v), pyoracle.fp(n))
+        assert np.array_equal(bits(n), n_ref[k]), k
+        t = np.zeros(3, np.float32)
+        b = np.zeros(3, np.float32)
+        lib.orc_kat_onb(pyoracle.fp(n), pyoracle.fp(t), pyoracle.fp(b))
+        assert np.array_equal(bits(t), t_ref[k]) and np.array_equal(bits(b), b_ref[k]), k
+
+
+def test_lambert_sample_dir(golden):
+    lib = pyoracle.lib()
+    m = pyoracle.mt(golden["lambert_seed"][0])
+    inp = f32(golden["lambert_in"]).reshape(-1, 3, 3)
+    wi_ref = np.asarray(golden["lambert_wi"], np.uint32).reshape(-1, 3)
+    pdf_ref = np.asarray(golden["lambert_pdf"], np.uint32)
+    for k in range(len(inp)):
+        ng, dpdu, dpdv = (np.ascontiguousarray(inp[k, q]) for q in range(3))
+        wi = np.zeros(3, np.float32)
+        pdf = np.zeros(1, np.float32)
+        lib.orc_kat_lambert(C.byref(m), pyoracle.fp(ng), pyoracle.fp(dpdu), pyoracle.fp(dpdv), pyoracle.fp(wi),
+                            pyoracle.fp(pdf))
+        assert np.array_equal(bits(wi), wi_ref[k]), k
+        assert bits(pdf)[0] == pdf_ref[k]
+
+
+def test_sphere_intersect_and_occluded(golden):
+    lib = pyoracle.lib()
+    inp = f32(golden["sphere_in"]).reshape(-1, 11)
+    hit = golden["sphere_hit"]
+    out = np.asarray(golden["sphere_out"], np.uint32).reshape(-1, 7)
+    occ = golden["sphere_occluded"]
+    for k in range(len(inp)):
+        o, d, c = (np.ascontiguousarray(inp[k, 3 * q:3 * q + 3]) for q in range(3))
+        r, tmax = float(inp[k, 9]), float(inp[k, 10])
+        res = np.zeros(7, np.float32)
+        h = lib.orc_kat_sphere(pyoracle.fp(o), pyoracle.fp(d), pyoracle.fp(c), C.c_float(r), pyoracle.fp(res))
+        assert h == hit[k], k
+        assert np.array_equal(bits(res), out[k]), (k, res, f32(out[k]))
+        assert lib.orc_kat_sphere_occluded(pyoracle.fp(o), pyoracle.fp(d), pyoracle.fp(c), C.c_float(r),
+                                           C.c_float(tmax)) == occ[k], k
+
+
+def test_box_intersect(golden):
+    lib = pyoracle.lib()
+    inp = f32(golden["box_in"]).reshape(-1, 12)
+    hit = golden["box_hit"]
+    out = np.asarray(golden["box_out"], np.uint32).reshape(-1, 2)
+    for k in range(len(inp)):
+        o, d, lo, hi = (np.ascontiguousarray(inp[k, 3 * q:3 * q + 3]) for q in range(4))
+        res = np.zeros(2, np.float32)
+        assert lib.orc_kat_box(pyoracle.fp(o), pyoracle.fp(d), pyoracle.fp(lo), pyoracle.fp(hi),
+                               pyoracle.fp(res)) == hit[k], k
+        assert np.array_equal(bits(res), out[k]), k
+
+
+def test_henyey_greenstein(golden):
+    lib = pyoracle.lib()
+    gs = f32(golden["hg_g"])
+    wo = f32(golden["hg_wo"]).reshape(len(gs), -1, 3)
+    wi_ref = np.asarray(golden["hg_wi"], np.uint32).reshape(len(gs), -1, 3)
+    ev_ref = np.asarray(golden["hg_eval"], np.uint32).reshape(len(gs), -1)
+    for gi, g in enumerate(gs):
+        m = pyoracle.mt(golden["hg_seed"][0])
+        for k in range(wo.shape[1]):
+            w = np.ascontiguousarray(wo[gi, k])
+            wi = np.zeros(3, np.float32)
+            ev = lib.orc_kat_hg(C.byref(m), C.c_float(g), pyoracle.fp(w), pyoracle.fp(wi))
+            assert np.array_equal(bits(wi), wi_ref[gi, k]), (g, k)
+            assert bits(np.float32(ev)) == ev_ref[gi, k], (g, k)
+
+
+def test_sample_wavelength(golden):
+    lib = pyoracle.lib()
+    m = pyoracle.mt(golden["wl_seed"][0])
+    inp = f32(golden["wl_in"]).reshape(-1, 2, 3)
+    ch = golden["wl_channel"]
+    pmf_ref = np.asarray(golden["wl_pmf"], np.uint32).reshape(-1, 3)
+    for k in range(len(inp)):
+        thr, alb = np.ascontiguousarray(inp[k, 0]), np.ascontiguousarray(inp[k, 1])
+        pmf = np.zeros(3, np.float32)
+        c = lib.orc_kat_wavelength(C.byref(m), pyoracle.fp(thr), pyoracle.fp(alb), pyoracle.fp(pmf))
+        assert c == ch[k], k
+        assert np.array_equal(bits(pmf), pmf_ref[k]), k
+
+
+def test_path_counters_match_reference_probe():
+    """SURVEY.md §6 / BASELINE.md: the reference, compiled and run by the survey on Cornell
+    800x600x16 GI(3), made 1.776 Scene::intersect and 0.752 Scene::occluded calls per
+    sample, and 84.5 ray-triangle tests per sample at 200x150.  The oracle's integrator
+    must reproduce those path statistics (they depend on every draw and every hit)."""
+    from xraytracer_amd import scenes
+    s = scenes.cornell(200, 150)
+    _, st = pyoracle.render(s, 200, 150, 16)
+    n = 200 * 150 * 16
+    assert round(st["segments"] / n, 3) == 1.776
+    assert round(st["shadow_rays"] / n, 3) in (0.751, 0.752)
+    assert round(st["tri_tests"] / n, 1) == 84.5
+    assert st["rejected"] == 0
