@@ -1,0 +1,204 @@
+"""bench.py — BASELINE.json metric: Msamples/s (whole node) + wall-clock at 800x600x1024 spp.
+
+One step = one full frame of the workload (default C2: Cornell box 800x600, 1024 spp,
+GIIntegrator(3)), rendered by the MI355X wavefront through libxrt_hip.so with the scene
+already resident in HBM.  With N GPUs (one process per GPU, torchrun) each rank renders the
+rows y % N == rank and the float3 framebuffers are summed to rank 0 with an RCCL reduce
+(exact: the other ranks contribute zeros).  Total work is fixed as N grows: "strong".
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--no-cpu]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Msamples/s (whole node) + wall-clock at 800×600×1024spp, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3        # vector FP32 spec
+
+# Algorithmic bytes per unit of work, from the data layout in DESIGN.md §Roofline:
+#   k_trace : per extension ray  — list 4 + state 4 + ray o,d 32 + hit record 16         = 56
+#             per shadow ray     — shadow o+tmax, d 32 + occlusion word 4                  = 36
+#   k_shade : per slot visit     — list 4 + state 4+4 + depth/k 8+8 + thr,rad 32+32
+#                                  + rng cursor/gen 8+8 + list out 4                       = 112
+#             per traced hit     — hit 16 + ray o,d 32 read + 32 write                     = 80
+#             per shadow ray     — record write o,d,contrib 48 + thr_prev 16 + read back
+#                                  contrib 16 + occlusion 4                                = 84
+#             per RNG draw       — 4 (tempered word) + 8 (amortised twist: 2*2496 B / 624) = 12
+#             per sample         — framebuffer read-modify-write 24
+B_TRACE_RAY, B_TRACE_SHADOW = 56, 36
+B_SHADE_VISIT, B_SHADE_HIT, B_SHADE_SHADOW, B_DRAW, B_SAMPLE = 112, 80, 84, 12, 24
+FLOP_PER_TRI_TEST = 40          # Moller-Trumbore with one correctly-rounded divide, approx.
+
+
+def env_int(k, d):
+    try:
+        return int(os.environ.get(k, d))
+    except ValueError:
+        return d
+
+
+def cpu_baseline(cfg_name, cfg, spp):
+    """The oracle (CPU restatement, bit-exact with the GPU path) on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from xraytracer_amd import scenes
+    threads = max(1, min(16, os.cpu_count() or 1))
+    s = scenes.build(cfg_name)
+    w, h = cfg["width"], cfg["height"]
+    t0 = time.perf_counter()
+    _, st = pyoracle.render(s, w, h, spp, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(w * h * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{cfg_name} scene {w}x{h} at {spp} spp (cost is linear in spp), oracle/oracle.c "
+                      f"with OpenMP over rows, {dt:.2f} s wall"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--spp", type=int, default=None, help="override spp (never for reported numbers)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-spp", type=int, default=32)
+    ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    from xraytracer_amd import abi, scenes
+    from xraytracer_amd.renderer import HipRenderer
+
+    world = env_int("WORLD_SIZE", 1)
+    rank = env_int("RANK", 0)
+    local = env_int("LOCAL_RANK", 0)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local)
+
+    cfg = dict(scenes.CONFIGS[args.config])
+    if args.spp:
+        cfg["spp"] = args.spp
+    W, H, SPP = cfg["width"], cfg["height"], cfg["spp"]
+    scene = scenes.build(args.config)
+    r = HipRenderer(SPP, device=local)
+    r.upload(scene)
+    fb = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
+    timing = not args.no_timing
+
+    def step(timed):
+        st = r.render_device(scene, W, H, fb.data_ptr(), shard_index=rank, shard_count=world,
+                             timing=timing and timed)
+        if dist is not None:
+            dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+        return st
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    agg = {k: 0.0 for k in ("segments", "shadow_rays", "draws", "samples", "iterations", "rejected")}
+    kms = np.zeros(abi.XRT_K_COUNT)
+    kl = np.zeros(abi.XRT_K_COUNT)
+    for _ in range(args.steps):
+        st = step(True)
+        for k in agg:
+            agg[k] += getattr(st, k)
+        kms += np.array(list(st.kernel_ms))
+        kl += np.array(list(st.launches))
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([agg["segments"], agg["shadow_rays"], agg["draws"], agg["samples"]],
+                           dtype=torch.float64, device=dev)
+        dist.all_reduce(tot)
+        agg["segments"], agg["shadow_rays"], agg["draws"], agg["samples"] = [float(x) for x in tot.tolist()]
+
+    if rank == 0:
+        total_samples = W * H * SPP * args.steps
+        value = total_samples / elapsed / 1e6
+        ms = elapsed / args.steps * 1e3
+        # roofline of the dominant kernel (per-launch algorithmic bytes / avg launch time)
+        roof = None
+        if timing and kms.sum() > 0:
+            bytes_k = {
+                abi.XRT_K_TRACE: B_TRACE_RAY * agg["segments"] + B_TRACE_SHADOW * agg["shadow_rays"],
+                abi.XRT_K_SHADE: (B_SHADE_VISIT * (agg["segments"] + agg["samples"] / max(1, world))
+                                  + B_SHADE_HIT * agg["segments"] + B_SHADE_SHADOW * agg["shadow_rays"]
+                                  + B_DRAW * agg["draws"] + B_SAMPLE * agg["samples"]),
+            }
+            if world > 1:   # per-rank kernel times, whole-job counters: use rank-0 share
+                bytes_k = {k: v / world for k, v in bytes_k.items()}
+            dom = max((abi.XRT_K_TRACE, abi.XRT_K_SHADE), key=lambda k: kms[k])
+            per_launch_bytes = bytes_k[dom] / max(1, kl[dom])
+            avg_s = kms[dom] / 1e3 / max(1, kl[dom])
+            achieved = per_launch_bytes / avg_s / 1e9
+            traffic = None
+            if os.path.exists(args.traffic):
+                try:
+                    tj = json.load(open(args.traffic))
+                    if tj.get("config") == args.config:
+                        traffic = tj.get("per_launch_bytes", {}).get(abi.KERNEL_NAMES[dom])
+                except (OSError, ValueError):
+                    traffic = None
+            roof = {"bound": "hbm", "kernel": "k_" + abi.KERNEL_NAMES[dom], "achieved": round(achieved, 2),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                    "traffic": traffic, "avg_launch_us": round(avg_s * 1e6, 3),
+                    "launches": int(kl[dom]), "algorithmic_bytes_per_launch": round(per_launch_bytes, 1)}
+            tri_tests = 0
+            if scene.desc.n_tris:
+                tri_tests = scene.desc.n_tris * (agg["segments"] + agg["shadow_rays"])   # upper bound
+            if tri_tests and kms[abi.XRT_K_TRACE] > 0:
+                roof["valu_tflops_trace_upper"] = round(
+                    tri_tests * FLOP_PER_TRI_TEST / (kms[abi.XRT_K_TRACE] / 1e3) / 1e12 / max(1, world), 3)
+            roof["kernel_ms_per_step"] = {abi.KERNEL_NAMES[i]: round(kms[i] / args.steps, 3)
+                                          for i in range(abi.XRT_K_COUNT)}
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{args.config}: {cfg['scene']} {W}x{H}, {SPP} spp, {cfg['integrator']}"
+                                   f"(maxDepth={cfg['max_depth']})",
+                       "width": W, "height": H, "spp": SPP, "integrator": cfg["integrator"],
+                       "max_depth": cfg["max_depth"], "global_batch": W * H * SPP,
+                       "parallelism": f"pixel rows y%{world} per GPU + RCCL reduce" if world > 1 else "1 GPU",
+                       "segments_per_sample": round(agg["segments"] / max(1, agg["samples"]), 4),
+                       "draws_per_sample": round(agg["draws"] / max(1, agg["samples"]), 4),
+                       "iterations_per_frame": round(agg["iterations"] / args.steps, 1)},
+            "roofline": roof,
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(args.config, cfg, args.cpu_spp)
+        print(json.dumps(out), flush=True)
+    r.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
