@@ -200,6 +200,8 @@ int xrt_test_trig(xrt_ctx* ctx, const float* x, uint32_t n, float* out);
  * restatement differs from the host values supplied by the caller in chunks. */
 int xrt_test_trig_draw_domain(xrt_ctx* ctx, uint32_t first_bits, uint32_t count, float* out_sin,
                               float* out_cos, float* out_r);
+/* glibc-logf/expf restatement on device over x[i]: out[2i] = logf, out[2i+1] = expf */
+int xrt_test_logexp(xrt_ctx* ctx, const float* x, uint32_t n, float* out);
 
 #ifdef __cplusplus
 }

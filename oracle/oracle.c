@@ -841,6 +841,14 @@ void orc_kat_light(orc_mt* m, const xrt_light* l, const float* pos, float* out) 
     st3(out + 5, L);
 }
 
+/* host glibc logf/expf over an array (the checker for the device restatement) */
+void orc_libm_logexpf(const float* x, uint32_t n, float* lg, float* ex) {
+    for (uint32_t i = 0; i < n; ++i) {
+        lg[i] = logf(x[i]);
+        ex[i] = expf(x[i]);
+    }
+}
+
 /* host glibc sinf/cosf over an array (the checker for the device restatement) */
 void orc_libm_sincosf(const float* x, uint32_t n, float* s, float* c) {
     for (uint32_t i = 0; i < n; ++i) {

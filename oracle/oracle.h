@@ -87,6 +87,7 @@ void orc_kat_light(orc_mt* m, const xrt_light* l, const float* pos, float* out);
 
 /* host libm sinf/cosf (checker for the device restatement) */
 void orc_libm_sincosf(const float* x, uint32_t n, float* s, float* c);
+void orc_libm_logexpf(const float* x, uint32_t n, float* lg, float* ex);
 
 #ifdef __cplusplus
 }

@@ -71,6 +71,7 @@ def lib():
         l.orc_kat_wavelength.restype = C.c_uint32
         l.orc_kat_light.argtypes = [C.POINTER(OrcMT), C.POINTER(abi.XrtLight), f32p, f32p]
         l.orc_libm_sincosf.argtypes = [f32p, C.c_uint32, f32p, f32p]
+        l.orc_libm_logexpf.argtypes = [f32p, C.c_uint32, f32p, f32p]
         _lib = l
     return _lib
 
@@ -140,6 +141,14 @@ def mt(seed) -> OrcMT:
     m = OrcMT()
     lib().orc_mt_seed(C.byref(m), seed)
     return m
+
+
+def libm_logexpf(x):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    lg = np.empty_like(x)
+    ex = np.empty_like(x)
+    lib().orc_libm_logexpf(fp(x), len(x), fp(lg), fp(ex))
+    return lg, ex
 
 
 def libm_sincosf(x):

@@ -99,6 +99,41 @@ def test_trig_general_arguments(gpu):
     assert np.array_equal(out[1::2].view(np.uint32), hc.view(np.uint32))
 
 
+def test_logf_restatement_on_vpt_domain(gpu):
+    """-log(max(1 - u, 0)) over every reachable draw u (VolumePathTracing free flights)."""
+    one = int(np.float32(1.0).view(np.uint32))
+    bits = np.arange(0, one, dtype=np.uint32)
+    r = bits.view(np.float32)
+    r = r[(r.astype(np.float64) * 4294967296.0) == np.floor(r.astype(np.float64) * 4294967296.0)]
+    x = np.maximum(np.float32(1.0) - r, np.float32(0.0)).astype(np.float32)
+    assert len(x) == 83886080
+    bad = 0
+    for k in range(0, len(x), 1 << 24):
+        xs = np.ascontiguousarray(x[k:k + (1 << 24)])
+        out = np.zeros(2 * len(xs), np.float32)
+        assert abi.lib().xrt_test_logexp(gpu, abi.fptr(xs), len(xs), abi.fptr(out)) == 0
+        lg, _ = pyoracle.libm_logexpf(xs)
+        bad += int(np.sum(out[0::2].view(np.uint32) != lg.view(np.uint32)))
+    assert bad == 0
+
+
+def test_expf_restatement_negative_range(gpu):
+    """expf over every 7th negative float down to -104 plus edge values (exp(-sigma*t))."""
+    lo = int(np.float32(-0.0).view(np.uint32))
+    hi = int(np.float32(-104.0).view(np.uint32))
+    bits = np.arange(lo, hi + 1, 7, dtype=np.uint64).astype(np.uint32)
+    edge = [0.0, -0.0, -np.inf, 1.0, 88.0, -103.5, float.fromhex("-0x1.f8cbb2p+5")]   # last: FMA-variant case
+    x = np.concatenate([bits.view(np.float32), np.array(edge, np.float32)])
+    bad = 0
+    for k in range(0, len(x), 1 << 24):
+        xs = np.ascontiguousarray(x[k:k + (1 << 24)])
+        out = np.zeros(2 * len(xs), np.float32)
+        assert abi.lib().xrt_test_logexp(gpu, abi.fptr(xs), len(xs), abi.fptr(out)) == 0
+        _, ex = pyoracle.libm_logexpf(xs)
+        bad += int(np.sum(out[1::2].view(np.uint32) != ex.view(np.uint32)))
+    assert bad == 0
+
+
 # ------------------------------------------------------------------ images ----
 def test_c1_cornell_gi_bit_exact(renderer):
     """Config C1 (Cornell 256x256x16, GIIntegrator(3)) — full framebuffer vs oracle."""
@@ -183,3 +218,21 @@ def test_triangle_light_and_two_lights(renderer):
     compare(img, ref)
     img, ref, _ = render_both(renderer, s, 64, 48, 4, integrator="direct")
     compare(img, ref)
+
+
+def test_c5_smoke_vpt(renderer):
+    """Config C5 family (synthetic density grid in a BoxMesh + quad light,
+    VolumePathTracing(10)) at reduced grid and image size."""
+    s = scenes.smoke(48, 36, n=32)
+    img, ref, st = render_both(renderer, s, 48, 36, 4)
+    compare(img, ref)
+    g = renderer.stats
+    assert g.draws == st["draws"] and g.segments == st["segments"] and g.stalled == st["stalled"] == 0
+
+
+def test_vpt_medium_walk_suspends_and_resumes(renderer):
+    """Many spp per pixel forces delta-tracking walks to cross RNG refills (suspend/resume)."""
+    s = scenes.smoke(12, 9, n=32)
+    img, ref, st = render_both(renderer, s, 12, 9, 96)
+    compare(img, ref)
+    assert renderer.stats.draws == st["draws"]

@@ -106,6 +106,7 @@ SIGNATURES = {
     "xrt_test_rng": (C.c_int, [C.c_void_p, u32p, C.c_uint32, C.c_uint32, C.c_uint32, f32p]),
     "xrt_test_trig": (C.c_int, [C.c_void_p, f32p, C.c_uint32, f32p]),
     "xrt_test_trig_draw_domain": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, f32p, f32p, f32p]),
+    "xrt_test_logexp": (C.c_int, [C.c_void_p, f32p, C.c_uint32, f32p]),
 }
 
 _lib = None

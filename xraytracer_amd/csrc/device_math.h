@@ -133,4 +133,81 @@ __device__ __forceinline__ float glibc_cosf(float y) {
     return __builtin_cosf(y);
 }
 
+// ---- glibc logf / expf ----------------------------------------------------------------
+// Used by VolumePathTracing's delta tracking: -std::log(max(1-u, 0)) and
+// analyticTransmittance = exp(-sigma*t) (Src/medium.cpp:51, 93-94; geometry.cpp:18-21).
+// Restatements of glibc 2.35 e_logf.c / e_expf.c (ARM optimized-routines) as the x86-64
+// FMA ifunc variant executes them (the host libm on FMA-capable CPUs); tables are
+// __logf_data and __exp2f_data read from the host libm.so.6.  Checked bit-for-bit against
+// host libm: logf on every 1-u of a reachable draw u, expf over all negative floats down
+// to -104 (tests/test_gpu_parity.py, oracle probe notes in DESIGN.md).
+static __constant__ const double kLogfTab[16][2] = {
+    {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
+    {0x1.49539f0f010b0p+0, -0x1.01eae7f513a67p-2}, {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
+    {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3}, {0x1.25e227b0b8ea0p+0, -0x1.1aa2bc79c8100p-3},
+    {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4}, {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4},
+    {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5}, {0x1.0000000000000p+0, 0x0.0p+0},
+    {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5}, {0x1.ca4b31f026aa0p-1, 0x1.c5e53aa362eb4p-4},
+    {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3}, {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d224770p-3},
+    {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2}, {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2}};
+__device__ __forceinline__ float glibc_logf(float x) {
+    const double Ln2 = 0x1.62e42fefa39efp-1, A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2,
+                 A2 = -0x1.ffffef20a4123p-2;
+    uint32_t ix = __float_as_uint(x);
+    if (ix == 0x3f800000u) return 0.0f;
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
+        if (ix * 2 == 0) return -__builtin_inff();
+        if (ix == 0x7f800000u) return x;
+        if ((ix & 0x80000000u) || ix * 2 >= 0xff000000u) return __builtin_nanf("");
+        ix = __float_as_uint(x * 0x1p23f);
+        ix -= 23u << 23;
+    }
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int i = (tmp >> (23 - 4)) % 16;
+    const int k = (int32_t)tmp >> 23;
+    const uint32_t iz = ix - (tmp & 0xff800000u);
+    const double invc = kLogfTab[i][0], logc = kLogfTab[i][1];
+    const double z = (double)__uint_as_float(iz);
+    const double r = __builtin_fma(z, invc, -1.0);
+    const double y0 = __builtin_fma((double)k, Ln2, logc);
+    const double r2 = r * r;
+    double y = __builtin_fma(A1, r, A2);
+    y = __builtin_fma(A0, r2, y);
+    y = __builtin_fma(y, r2, y0 + r);
+    return (float)y;
+}
+static __constant__ const uint64_t kExp2fTab[32] = {
+    0x3ff0000000000000, 0x3fefd9b0d3158574, 0x3fefb5586cf9890f, 0x3fef9301d0125b51, 0x3fef72b83c7d517b,
+    0x3fef54873168b9aa, 0x3fef387a6e756238, 0x3fef1e9df51fdee1, 0x3fef06fe0a31b715, 0x3feef1a7373aa9cb,
+    0x3feedea64c123422, 0x3feece086061892d, 0x3feebfdad5362a27, 0x3feeb42b569d4f82, 0x3feeab07dd485429,
+    0x3feea47eb03a5585, 0x3feea09e667f3bcd, 0x3fee9f75e8ec5f74, 0x3feea11473eb0187, 0x3feea589994cce13,
+    0x3feeace5422aa0db, 0x3feeb737b0cdc5e5, 0x3feec49182a3f090, 0x3feed503b23e255d, 0x3feee89f995ad3ad,
+    0x3feeff76f2fb5e47, 0x3fef199bdd85529c, 0x3fef3720dcef9069, 0x3fef5818dcfba487, 0x3fef7c97337b9b5f,
+    0x3fefa4afa2a490da, 0x3fefd0765b6e4540};
+__device__ __forceinline__ float glibc_expf(float x) {
+    const double SHIFT = 0x1.8p+52, InvLn2N = 0x1.71547652b82fep+5, C0 = 0x1.c6af84b912394p-20,
+                 C1 = 0x1.ebfce50fac4f3p-13, C2 = 0x1.62e42ff0c52d6p-6;
+    const double xd = (double)x;
+    const uint32_t top = __float_as_uint(x) >> 20;
+    const uint32_t abstop = top & 0x7ff;
+    if (abstop >= (__float_as_uint(88.0f) >> 20)) {
+        if (__float_as_uint(x) == 0xff800000u) return 0.0f;
+        if (abstop >= (0x7f800000u >> 20)) return x + x;
+        if (x > 0x1.62e42ep6f) return __builtin_inff();
+        if (x < -0x1.9fe368p6f) return 0.0f;
+    }
+    double kd = __builtin_fma(InvLn2N, xd, SHIFT);
+    const uint64_t ki = (uint64_t)__double_as_longlong(kd);
+    kd -= SHIFT;
+    const double r = __builtin_fma(InvLn2N, xd, -kd);
+    uint64_t t = kExp2fTab[ki % 32];
+    t += ki << (52 - 5);
+    const double s = __longlong_as_double((long long)t);
+    const double zz = __builtin_fma(C0, r, C1);
+    const double r2 = r * r;
+    double y = __builtin_fma(C2, r, 1.0);
+    y = __builtin_fma(zz, r2, y);
+    return (float)(y * s);
+}
+
 }  // namespace xrt

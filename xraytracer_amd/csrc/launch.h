@@ -17,4 +17,5 @@ hipError_t launch_test_rng(const uint32_t* seeds, uint32_t n_seeds, uint32_t ski
                            uint32_t* rings, hipStream_t st);
 hipError_t launch_test_trig(const float* x, uint32_t n, float* out, hipStream_t st);
 hipError_t launch_test_trig_domain(uint32_t first, uint32_t count, float* s, float* c, float* r, hipStream_t st);
+hipError_t launch_test_logexp(const float* x, uint32_t n, float* out, hipStream_t st);
 }  // namespace xrt

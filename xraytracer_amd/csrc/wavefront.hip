@@ -460,6 +460,127 @@ __device__ __forceinline__ void camera_ray(const KParams& P, float u, float v, v
     o = mk(x[12], x[13], x[14]);
 }
 
+// ==================================================================== medium ====
+// DensityGrid::getDensity = OpenVDB BoxSampler::wsSample (Src/grid.h:71-77): index-space
+// position in double, floor, trilinear lerps a + float((b - a) * w) (z, then y, then x),
+// background 0 outside the voxels.
+__device__ __forceinline__ float grid_value(const DMedium& M, int i, int j, int k) {
+    if (i < 0 || j < 0 || k < 0 || i >= M.nx || j >= M.ny || k >= M.nz) return 0.0f;
+    return M.density[((size_t)k * M.ny + (size_t)j) * M.nx + (size_t)i];
+}
+__device__ __forceinline__ float vdb_lerp(float a, float b, double w) { return a + (float)((double)(b - a) * w); }
+__device__ float medium_density(const DMedium& M, v3 p) {
+    const double inv = 1.0 / (double)M.voxel_size;
+    const double xi = ((double)p.x - (double)M.origin[0]) * inv;
+    const double yi = ((double)p.y - (double)M.origin[1]) * inv;
+    const double zi = ((double)p.z - (double)M.origin[2]) * inv;
+    const double fx = __builtin_floor(xi), fy = __builtin_floor(yi), fz = __builtin_floor(zi);
+    const int i = (int)fx, j = (int)fy, k = (int)fz;
+    const double u = xi - fx, v = yi - fy, w = zi - fz;
+    const float d000 = grid_value(M, i, j, k), d001 = grid_value(M, i, j, k + 1);
+    const float d010 = grid_value(M, i, j + 1, k), d011 = grid_value(M, i, j + 1, k + 1);
+    const float d100 = grid_value(M, i + 1, j, k), d101 = grid_value(M, i + 1, j, k + 1);
+    const float d110 = grid_value(M, i + 1, j + 1, k), d111 = grid_value(M, i + 1, j + 1, k + 1);
+    const float g = vdb_lerp(vdb_lerp(vdb_lerp(d000, d001, w), vdb_lerp(d010, d011, w), v),
+                             vdb_lerp(vdb_lerp(d100, d101, w), vdb_lerp(d110, d111, w), v), u);
+    return M.multiplier * g;   // HeterogeneousMedium::getDensity (Src/medium.cpp:24-27)
+}
+
+// Medium::sampleWavelength + DiscreteEmpiricalDistribution1D (Src/medium.h:102-115,
+// Src/sampler.h:53-94).  lower_bound past the end is UB in the reference; clamped to 2.
+__device__ __forceinline__ uint32_t sample_wavelength(v3 thr, v3 albedo, Rng& rng, v3& pmf) {
+    const v3 ta = thr * albedo;
+    const float sum = ((0.0f + ta.x) + ta.y) + ta.z;
+    const float c1 = 0.0f + ta.x / sum;
+    const float c2 = c1 + ta.y / sum;
+    const float c3 = c2 + ta.z / sum;
+    pmf = mk(c1 - 0.0f, c2 - c1, c3 - c2);
+    const float u = rng.next();
+    int x = 0;
+    if (0.0f < u) {
+        x = 1;
+        if (c1 < u) {
+            x = 2;
+            if (c2 < u) x = (c3 < u) ? 4 : 3;
+        }
+    }
+    if (x == 0) x = 1;
+    if (x == 4) x = 3;
+    return (uint32_t)(x - 1);
+}
+
+// HenyeyGreenstein::sampleDirection (Src/medium.h:37-67); getNext2D = (2nd, 1st draw)
+__device__ void hg_sample(float g, v3 wo, Rng& rng, v3& wi) {
+    const float d1 = rng.next();
+    const float d2 = rng.next();
+    const float u0 = d2, u1 = d1;
+    float cosTheta;
+    if (__builtin_fabs((double)g) < 1e-3) {
+        cosTheta = 2.0f * u0 - 1.0f;
+    } else {
+        const float sqrTerm = (1.0f - g * g) / (1.0f - g + 2.0f * g * u0);
+        cosTheta = (1.0f + g * g - sqrTerm * sqrTerm) / (2.0f * g);
+    }
+    const float sinTheta = __builtin_sqrtf(smax(1.0f - cosTheta * cosTheta, 0.0f));
+    const float phi = 2.0f * kPI * u1;
+    const v3 wl = mk(glibc_cosf(phi) * sinTheta, cosTheta, glibc_sinf(phi) * sinTheta);
+    v3 t, b;
+    onb(wo, t, b);
+    wi = local_to_world(wl, t, wo, b);
+}
+
+__device__ __forceinline__ v3 vexp(v3 a) { return mk(glibc_expf(a.x), glibc_expf(a.y), glibc_expf(a.z)); }
+__device__ __forceinline__ bool isnan3(v3 a) {
+    return __builtin_isnan(a.x) || __builtin_isnan(a.y) || __builtin_isnan(a.z);
+}
+
+// HeterogeneousMedium::sampleMedium — delta tracking with spectral MIS (Src/medium.cpp:
+// 45-133), resumable: returns 0 = left the medium, 1 = real scattering, 2 = suspended
+// because fewer than 8 RNG words remain (the slot resumes after the next refill).
+// `t`, `tt` (throughput_tracking) and `sa` (sigma_a) carry the loop state.
+__device__ int delta_track(const KParams& P, v3 o, v3 d, v3 thr, float& t, float t1, v3& tt, v3& sa, Rng& rng,
+                           uint32_t g, v3& pos, v3& dir, v3& tm) {
+    const DMedium& M = P.medium;
+    const float majorant = M.majorant, invMajorant = M.inv_majorant;
+    const v3 vmaj = mk(majorant, majorant, majorant);
+    const v3 absorb = ld3(M.absorption), scatter = ld3(M.scattering);
+    for (;;) {
+        if (g - rng.c < 8u) return 2;
+        v3 pmf;
+        const uint32_t channel = sample_wavelength(thr * tt, (vmaj - sa) * invMajorant, rng, pmf);
+        const float s = -glibc_logf(smax(1.0f - rng.next(), 0.0f)) * invMajorant;
+        t += s;
+        if (t > t1 - kRAY_EPS) {
+            pos = ray_at(o, d, t1 + kRAY_EPS);
+            dir = d;
+            const float dist = s - (t - (t1 - kRAY_EPS));
+            const v3 tr = vexp((-vmaj) * dist);
+            const v3 pdf = pmf * tr;
+            tt = tt * (tr / (pdf.x + pdf.y + pdf.z));
+            tm = isnan3(tt) ? mk(0, 0, 0) : tt;
+            return 0;
+        }
+        const float density = medium_density(M, ray_at(o, d, t));
+        const v3 sigma_s = scatter * density;
+        sa = absorb * density;
+        const v3 sigma_n = (vmaj - sa) - sigma_s;
+        const v3 P_s = sigma_s / (sigma_s + sigma_n);
+        const v3 P_n = sigma_n / (sigma_s + sigma_n);
+        if (rng.next() < comp(P_s, channel)) {
+            pos = ray_at(o, d, t);
+            hg_sample(M.g, d, rng, dir);
+            const v3 tr = vexp((-vmaj) * s);
+            const v3 pdf = (pmf * (tr * majorant)) * P_s;
+            tt = tt * ((tr * sigma_s) / (pdf.x + pdf.y + pdf.z));
+            tm = isnan3(tt) ? mk(0, 0, 0) : tt;
+            return 1;
+        }
+        const v3 tr = vexp((-vmaj) * s);
+        const v3 pdf = (pmf * (tr * majorant)) * P_n;
+        tt = tt * ((tr * sigma_n) / (pdf.x + pdf.y + pdf.z));
+    }
+}
+
 // =================================================================== k_shade ====
 template <int SCN, int INTEG>
 __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __restrict__ list,
@@ -482,7 +603,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
             uint32_t k = P.sample_k[s];
             v3 thr = xyz(P.thr[s]), rad = xyz(P.rad[s]);
             v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
-            uint32_t nseg = 0, nsh = 0, nrej = 0;
+            uint32_t nseg = 0, nsh = 0, nrej = 0, nstall = 0;
             bool finalize = false;
 
             // ---- 1. resolve the previous bounce's NEE with the shadow-ray results
@@ -511,8 +632,78 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
                 if (st & ST_END) finalize = true;
             }
 
-            // ---- 2. shade the traced extension ray
-            if (st & ST_RAY) {
+            // ---- 2. shade the traced extension ray (or resume a suspended medium walk)
+            if (INTEG == XRT_INTEGRATOR_VPT && (st & (ST_RAY | ST_MEDIUM))) {
+                // VolumePathTracing::integrate loop body (Src/integrator.h:418-469)
+                o = xyz(P.ray_o[s]);
+                d = xyz(P.ray_d[s]);
+                bool walk = false;
+                float mt = 0.0f, mt1 = 0.0f;
+                v3 tt = mk(1, 1, 1), sa = mk(0, 0, 0);
+                if (st & ST_MEDIUM) {
+                    st &= ~ST_MEDIUM;
+                    const f4 m1 = P.med[s], m2 = P.med2[s];
+                    mt = m1.x, mt1 = m1.y, sa = mk(m1.z, m1.w, m2.w), tt = xyz(m2);
+                    walk = true;
+                } else {
+                    st &= ~ST_RAY;
+                    ++nseg;
+                    Surf S;
+                    float t1;
+                    const f4 h = P.hit[s];
+                    const int obj = surface<SCN>(P, s, o, d, h, S, t1);
+                    if (obj < 0) {
+                        rad = rad + (thr * mk(0.0f, 0.0f, 0.0f)) * (float)(depth != 0);
+                        finalize = true;
+                    } else {
+                        bool alive = true;
+                        if (depth > 0) {
+                            const float p = smin((thr.x + thr.y + thr.z) / 3.0f, 1.0f);
+                            if (rng.next() >= p) alive = false, finalize = true;
+                            else thr = thr / mk(p, p, p);
+                        }
+                        const DObj ob = P.objs[obj];
+                        if (alive && ob.light >= 0) {
+                            rad = rad + thr * light_Le(P.lights[ob.light], S.ns, d);
+                            alive = false, finalize = true;
+                        }
+                        if (alive) {
+                            if (ob.medium >= 0) {
+                                // sampleMedium entry (Src/medium.cpp:47-52): t = info.t
+                                mt = h.x, mt1 = t1;
+                                sa = ld3(P.medium.absorption) * medium_density(P.medium, ray_at(o, d, mt));
+                                walk = true;
+                            } else {
+                                // neither light nor medium: the reference never advances this
+                                // ray (endless loop); stop the path and count it.
+                                ++nstall;
+                                finalize = true;
+                            }
+                        }
+                    }
+                }
+                if (walk) {
+                    v3 pos, dir, tm;
+                    const int r = delta_track(P, o, d, thr, mt, mt1, tt, sa, rng, g, pos, dir, tm);
+                    if (r == 2) {
+                        st |= ST_MEDIUM;
+                        P.med[s] = make_float4(mt, mt1, sa.x, sa.y);
+                        P.med2[s] = make_float4(tt.x, tt.y, tt.z, sa.z);
+                    } else {
+                        o = pos;
+                        d = dir;
+                        thr = thr * tm;
+                        if (r == 1) ++depth;
+                        if (depth < P.max_depth) {
+                            st |= ST_RAY;
+                            P.ray_o[s] = pk(o);
+                            P.ray_d[s] = pk(d);
+                        } else {
+                            finalize = true;
+                        }
+                    }
+                }
+            } else if (st & ST_RAY) {
                 st &= ~ST_RAY;
                 ++nseg;
                 o = xyz(P.ray_o[s]);
@@ -685,6 +876,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
             if (nseg) P.c_seg[s] += nseg;
             if (nsh) P.c_shadow[s] += nsh;
             if (nrej) P.c_rej[s] += nrej;
+            if (nstall) P.c_stall[s] += nstall;
         }
         // ---- 4. compaction: ballot + prefix count, one atomic per wave
         const bool keep = valid && !(st & ST_DONE);
@@ -788,6 +980,14 @@ __global__ void k_test_trig_domain(uint32_t first, uint32_t count, float* out_si
     out_cos[i] = glibc_cosf(phi);
 }
 
+__global__ void k_test_logexp(const float* x, uint32_t n, float* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        out[2 * i] = glibc_logf(x[i]);
+        out[2 * i + 1] = glibc_expf(x[i]);
+    }
+}
+
 // ================================================================== launchers ====
 }  // namespace xrt
 
@@ -826,6 +1026,9 @@ static hipError_t shade_i(const KParams& P, const uint32_t* list, const uint32_t
     if (P.integrator == XRT_INTEGRATOR_DIRECT)
         hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_DIRECT>), dim3(blocks), dim3(kBlock), 0, st, P, list,
                            count, out, out_count);
+    else if (P.integrator == XRT_INTEGRATOR_VPT)
+        hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_VPT>), dim3(blocks), dim3(kBlock), 0, st, P, list, count,
+                           out, out_count);
     else
         hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_GI>), dim3(blocks), dim3(kBlock), 0, st, P, list, count,
                            out, out_count);
@@ -861,6 +1064,11 @@ hipError_t launch_test_trig(const float* x, uint32_t n, float* out, hipStream_t 
 
 hipError_t launch_test_trig_domain(uint32_t first, uint32_t count, float* s, float* c, float* r, hipStream_t st) {
     hipLaunchKernelGGL(k_test_trig_domain, dim3((count + 255) / 256), dim3(256), 0, st, first, count, s, c, r);
+    return hipGetLastError();
+}
+
+hipError_t launch_test_logexp(const float* x, uint32_t n, float* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_test_logexp, dim3((n + 255) / 256), dim3(256), 0, st, x, n, out);
     return hipGetLastError();
 }
 

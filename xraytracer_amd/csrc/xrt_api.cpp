@@ -292,8 +292,11 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     if (!c->has_scene || !c->has_camera) return set_err(c, XRT_ERR_STATE, "upload a scene and set a camera first");
     if (p->width == 0 || p->height == 0 || p->shard_count == 0 || p->shard_index >= p->shard_count)
         return set_err(c, XRT_ERR_INVALID, "bad image size or shard");
-    if (p->integrator != XRT_INTEGRATOR_GI && p->integrator != XRT_INTEGRATOR_DIRECT)
-        return set_err(c, XRT_ERR_UNSUPPORTED, "integrator not implemented");
+    if (p->integrator != XRT_INTEGRATOR_GI && p->integrator != XRT_INTEGRATOR_DIRECT &&
+        p->integrator != XRT_INTEGRATOR_VPT)
+        return set_err(c, XRT_ERR_INVALID, "unknown integrator");
+    if (p->integrator == XRT_INTEGRATOR_VPT && !c->has_medium)
+        return set_err(c, XRT_ERR_STATE, "VolumePathTracing needs xrt_set_medium first");
     HIPCHK(c, hipSetDevice(c->device));
     const uint32_t rows = shard_rows(p->height, p->shard_index, p->shard_count);
     const size_t n = (size_t)rows * p->width;
@@ -370,7 +373,10 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     HIPCHK(c, launch(XRT_K_SEED, [&] { return launch_seed(P, lists[0], counts + 0, counts + 1, c->stream); }));
 
     const uint32_t blocks = (uint32_t)std::min<size_t>((n + 255) / 256, 8192);
-    const uint64_t cap_iters = (uint64_t)p->spp * (p->max_depth + 2) + 16;
+    // GI/Direct: at most max_depth + 1 shade passes per sample; VPT walks are unbounded
+    // (null collisions, suspensions), so only the live-slot poll ends the loop there.
+    const uint64_t cap_iters = p->integrator == XRT_INTEGRATOR_VPT ? (uint64_t)p->spp * 100000ull + 1000000ull
+                                                                    : (uint64_t)p->spp * (p->max_depth + 2) + 16;
     // asynchronous termination polling: every kPoll iterations copy the live-slot count to
     // pinned memory; block on a poll only when the host runs kAhead iterations ahead.
     constexpr uint64_t kPoll = 16, kAhead = 64;
@@ -475,6 +481,20 @@ int xrt_test_trig(xrt_ctx* c, const float* x, uint32_t n, float* out) {
     if (e == hipSuccess) e = hipMemcpy(out, dout.p, (size_t)n * 8, hipMemcpyDeviceToHost);
     free_buf(dx), free_buf(dout);
     return e == hipSuccess ? XRT_OK : hip_err(c, e, "xrt_test_trig");
+}
+
+int xrt_test_logexp(xrt_ctx* c, const float* x, uint32_t n, float* out) {
+    if (!c || !x || !out) return XRT_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    DevBuf dx, dout;
+    int rc;
+    if ((rc = ensure(c, dx, (size_t)n * 4 + 16)) || (rc = ensure(c, dout, (size_t)n * 8 + 16))) return rc;
+    hipError_t e = hipMemcpy(dx.p, x, (size_t)n * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_test_logexp(as<float>(dx), n, as<float>(dout), c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, dout.p, (size_t)n * 8, hipMemcpyDeviceToHost);
+    free_buf(dx), free_buf(dout);
+    return e == hipSuccess ? XRT_OK : hip_err(c, e, "xrt_test_logexp");
 }
 
 int xrt_test_trig_draw_domain(xrt_ctx* c, uint32_t first, uint32_t count, float* out_sin, float* out_cos, float* out_r) {
