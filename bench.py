@@ -75,7 +75,7 @@ def main():
     import numpy as np
     import torch
 
-    from xraytracer_amd import abi, scenes
+    from xraytracer_amd import abi, distributed, scenes
     from xraytracer_amd.renderer import HipRenderer
 
     world = env_int("WORLD_SIZE", 1)
@@ -103,8 +103,7 @@ def main():
     def step(timed):
         st = r.render_device(scene, W, H, fb.data_ptr(), shard_index=rank, shard_count=world,
                              timing=timing and timed)
-        if dist is not None:
-            dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+        distributed.reduce_framebuffer(fb, dist)
         return st
 
     for _ in range(args.warmup):
@@ -129,9 +128,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = distributed.max_over_ranks(elapsed, dist, device=dev)
         tot = torch.tensor([agg["segments"], agg["shadow_rays"], agg["draws"], agg["samples"]],
                            dtype=torch.float64, device=dev)
         dist.all_reduce(tot)
