@@ -31,8 +31,12 @@ FP32_PEAK_TFLOPS = 157.3        # vector FP32 spec
 #                                  contrib 16 + occlusion 4                                = 84
 #             per RNG draw       — 4 (tempered word) + 8 (amortised twist: 2*2496 B / 624) = 12
 #             per sample         — framebuffer read-modify-write 24
+#   k_step  : per segment        — list 4 + state 4+4 + depth/k 8+8 + thr,rad 32+32
+#                                  + ray o,d 32+32 + rng cursor/gen 8+8 + list out 4       = 176
+#             (+ per RNG draw 12, per sample 24 as above; the scene is read from LDS)
 B_TRACE_RAY, B_TRACE_SHADOW = 56, 36
 B_SHADE_VISIT, B_SHADE_HIT, B_SHADE_SHADOW, B_DRAW, B_SAMPLE = 112, 80, 84, 12, 24
+B_STEP_SEG = 176
 FLOP_PER_TRI_TEST = 40          # Moller-Trumbore with one correctly-rounded divide, approx.
 
 
@@ -69,6 +73,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=32)
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--schedule", default="auto", choices=("auto", "wavefront"))
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     args = ap.parse_args()
 
@@ -102,7 +107,7 @@ def main():
 
     def step(timed):
         st = r.render_device(scene, W, H, fb.data_ptr(), shard_index=rank, shard_count=world,
-                             timing=timing and timed)
+                             timing=timing and timed, schedule=args.schedule)
         distributed.reduce_framebuffer(fb, dist)
         return st
 
@@ -146,10 +151,11 @@ def main():
                 abi.XRT_K_SHADE: (B_SHADE_VISIT * (agg["segments"] + agg["samples"] / max(1, world))
                                   + B_SHADE_HIT * agg["segments"] + B_SHADE_SHADOW * agg["shadow_rays"]
                                   + B_DRAW * agg["draws"] + B_SAMPLE * agg["samples"]),
+                abi.XRT_K_STEP: B_STEP_SEG * agg["segments"] + B_DRAW * agg["draws"] + B_SAMPLE * agg["samples"],
             }
             if world > 1:   # per-rank kernel times, whole-job counters: use rank-0 share
                 bytes_k = {k: v / world for k, v in bytes_k.items()}
-            dom = max((abi.XRT_K_TRACE, abi.XRT_K_SHADE), key=lambda k: kms[k])
+            dom = max((abi.XRT_K_TRACE, abi.XRT_K_SHADE, abi.XRT_K_STEP), key=lambda k: kms[k])
             per_launch_bytes = bytes_k[dom] / max(1, kl[dom])
             avg_s = kms[dom] / 1e3 / max(1, kl[dom])
             achieved = per_launch_bytes / avg_s / 1e9
@@ -168,9 +174,10 @@ def main():
             tri_tests = 0
             if scene.desc.n_tris:
                 tri_tests = scene.desc.n_tris * (agg["segments"] + agg["shadow_rays"])   # upper bound
-            if tri_tests and kms[abi.XRT_K_TRACE] > 0:
+            tk = abi.XRT_K_STEP if kl[abi.XRT_K_STEP] else abi.XRT_K_TRACE
+            if tri_tests and kms[tk] > 0:
                 roof["valu_tflops_trace_upper"] = round(
-                    tri_tests * FLOP_PER_TRI_TEST / (kms[abi.XRT_K_TRACE] / 1e3) / 1e12 / max(1, world), 3)
+                    tri_tests * FLOP_PER_TRI_TEST / (kms[tk] / 1e3) / 1e12 / max(1, world), 3)
             roof["kernel_ms_per_step"] = {abi.KERNEL_NAMES[i]: round(kms[i] / args.steps, 3)
                                           for i in range(abi.XRT_K_COUNT)}
         out = {
@@ -184,7 +191,8 @@ def main():
                        "parallelism": f"pixel rows y%{world} per GPU + RCCL reduce" if world > 1 else "1 GPU",
                        "segments_per_sample": round(agg["segments"] / max(1, agg["samples"]), 4),
                        "draws_per_sample": round(agg["draws"] / max(1, agg["samples"]), 4),
-                       "iterations_per_frame": round(agg["iterations"] / args.steps, 1)},
+                       "iterations_per_frame": round(agg["iterations"] / args.steps, 1),
+                       "schedule": "fused k_step" if kl[abi.XRT_K_STEP] else "wavefront k_shade+k_trace"},
             "roofline": roof,
             "cpu_baseline": None,
         }

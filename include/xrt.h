@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 1
+#define XRT_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------------------- */
 enum {
@@ -103,7 +103,11 @@ typedef struct {
 
 /* ---- render parameters --------------------------------------------------------------- */
 enum { XRT_INTEGRATOR_GI = 0, XRT_INTEGRATOR_DIRECT = 1, XRT_INTEGRATOR_VPT = 2 };
-enum { XRT_FLAG_TIMING = 1u };   /* time every kernel with HIP events (xrt_stats.kernel_ms) */
+enum {
+    XRT_FLAG_TIMING = 1u,      /* time every kernel with HIP events (xrt_stats.kernel_ms)     */
+    XRT_FLAG_WAVEFRONT = 2u    /* force the multi-pass schedule (k_shade + k_trace) even when
+                                  the scene fits the fused LDS-resident schedule (k_step)     */
+};
 
 typedef struct {
     int32_t integrator;      /* XRT_INTEGRATOR_*                                        */
@@ -115,7 +119,7 @@ typedef struct {
     uint32_t flags;          /* XRT_FLAG_*                                              */
 } xrt_render_params;
 
-enum { XRT_K_SEED = 0, XRT_K_TRACE = 1, XRT_K_SHADE = 2, XRT_K_FINISH = 3, XRT_K_COUNT = 4 };
+enum { XRT_K_SEED = 0, XRT_K_TRACE = 1, XRT_K_SHADE = 2, XRT_K_FINISH = 3, XRT_K_STEP = 4, XRT_K_COUNT = 5 };
 
 typedef struct {
     double wall_ms;              /* host wall clock of the render call (upload excluded) */
@@ -126,7 +130,7 @@ typedef struct {
     uint64_t shadow_rays;        /* Scene::occluded calls                                  */
     uint64_t draws;              /* RNG draws (Sampler::getNext1D)                         */
     uint64_t rejected;           /* samples dropped by the NaN/Inf/negative check          */
-    uint64_t iterations;         /* trace+shade pass pairs                                 */
+    uint64_t iterations;         /* trace+shade pass pairs, or k_step launches             */
     uint64_t path_slots;         /* slots in flight (pixels of this shard)                 */
     uint64_t trace_slot_visits;  /* sum over trace launches of active slots                */
     uint64_t stalled;            /* paths stopped by the VPT no-progress guard             */

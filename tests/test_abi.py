@@ -27,7 +27,7 @@ def test_binding_covers_header():
 
 
 def test_abi_version():
-    assert abi.lib().xrt_abi_version() == 1
+    assert abi.lib().xrt_abi_version() == abi.XRT_ABI_VERSION
 
 
 def test_null_arguments_are_rejected_without_a_gpu():

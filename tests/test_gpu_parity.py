@@ -34,11 +34,21 @@ def renderer():
     r.close()
 
 
-def render_both(r, scene, w, h, spp, **kw):
+@pytest.fixture(params=["auto", "wavefront"])
+def sched(request):
+    """Both device schedules: "auto" runs the fused LDS-resident k_step for scenes that fit
+    (every scene below except the C4 sphere mesh), "wavefront" forces k_shade + k_trace."""
+    return request.param
+
+
+def render_both(r, scene, w, h, spp, schedule="auto", **kw):
     r.spp = spp
     r._uploaded = None
-    img = r.render(scene, w, h, **kw)
+    img = r.render(scene, w, h, schedule=schedule, **kw)
     ref, st = pyoracle.render(scene, w, h, spp, **kw)
+    steps = r.stats.launches[abi.XRT_K_STEP]
+    if schedule == "wavefront":
+        assert steps == 0
     return img, ref, st
 
 
@@ -135,43 +145,44 @@ def test_expf_restatement_negative_range(gpu):
 
 
 # ------------------------------------------------------------------ images ----
-def test_c1_cornell_gi_bit_exact(renderer):
+def test_c1_cornell_gi_bit_exact(renderer, sched):
     """Config C1 (Cornell 256x256x16, GIIntegrator(3)) — full framebuffer vs oracle."""
     s = scenes.cornell(256, 256)
-    img, ref, st = render_both(renderer, s, 256, 256, 16)
+    img, ref, st = render_both(renderer, s, 256, 256, 16, schedule=sched)
     compare(img, ref)
     g = renderer.stats
+    assert (g.launches[abi.XRT_K_STEP] > 0) == (sched == "auto")
     assert (g.segments, g.shadow_rays, g.draws, g.rejected) == (st["segments"], st["shadow_rays"], st["draws"],
                                                                 st["rejected"])
 
 
-def test_cornell_gi_nonsquare_and_depths(renderer):
+def test_cornell_gi_nonsquare_and_depths(renderer, sched):
     s = scenes.cornell(80, 60)
     for depth in (1, 2, 5):
-        img, ref, st = render_both(renderer, s, 80, 60, 8, max_depth=depth)
+        img, ref, st = render_both(renderer, s, 80, 60, 8, max_depth=depth, schedule=sched)
         compare(img, ref)
         assert renderer.stats.draws == st["draws"]
 
 
-def test_cornell_direct(renderer):
+def test_cornell_direct(renderer, sched):
     s = scenes.cornell(96, 72)
-    img, ref, _ = render_both(renderer, s, 96, 72, 8, integrator="direct")
+    img, ref, _ = render_both(renderer, s, 96, 72, 8, integrator="direct", schedule=sched)
     compare(img, ref)
 
 
 @pytest.mark.parametrize("wh", [(1, 1), (7, 3), (65, 33)])
-def test_edge_sizes(renderer, wh):
+def test_edge_sizes(renderer, wh, sched):
     w, h = wh
     s = scenes.cornell(w, h)
-    img, ref, _ = render_both(renderer, s, w, h, 3)
+    img, ref, _ = render_both(renderer, s, w, h, 3, schedule=sched)
     compare(img, ref)
 
 
-def test_spp_one_and_depth_zero(renderer):
+def test_spp_one_and_depth_zero(renderer, sched):
     s = scenes.cornell(40, 30)
-    img, ref, _ = render_both(renderer, s, 40, 30, 1)
+    img, ref, _ = render_both(renderer, s, 40, 30, 1, schedule=sched)
     compare(img, ref)
-    img, ref, _ = render_both(renderer, s, 40, 30, 4, max_depth=0)
+    img, ref, _ = render_both(renderer, s, 40, 30, 4, max_depth=0, schedule=sched)
     assert np.all(img == 0) and np.all(ref == 0)
 
 
@@ -190,10 +201,10 @@ def test_shards_reassemble_exactly(renderer):
     assert np.array_equal(acc, full)
 
 
-def test_c3_spheres_direct(renderer):
+def test_c3_spheres_direct(renderer, sched):
     """Config C3 scene (1000 spheres + sphere light, DirectIntegrator) at reduced size."""
     s = scenes.spheres(160, 90)
-    img, ref, st = render_both(renderer, s, 160, 90, 4)
+    img, ref, st = render_both(renderer, s, 160, 90, 4, schedule=sched)
     compare(img, ref)
     assert renderer.stats.shadow_rays == st["shadow_rays"]
 
@@ -203,9 +214,10 @@ def test_c4_sphere_mesh_gi(renderer):
     s = scenes.cornell_spheremesh(64, 36, n_theta=24, n_phi=24)
     img, ref, _ = render_both(renderer, s, 64, 36, 4)
     compare(img, ref)
+    assert renderer.stats.launches[abi.XRT_K_STEP] == 0   # too large for LDS: multi-pass schedule
 
 
-def test_triangle_light_and_two_lights(renderer):
+def test_triangle_light_and_two_lights(renderer, sched):
     s = scenes.SceneBundle()
     s.load_obj(scenes.CORNELL_OBJ)
     s.add_quad_light("QuadLight", (343.0, 548.0, 227.0), (343.0, 548.0, 332.0), (213.0, 548.0, 227.0),
@@ -214,26 +226,26 @@ def test_triangle_light_and_two_lights(renderer):
                          (10.0, 5.0, 2.0))
     s.flatten()
     s.camera = scenes.pinhole(scenes.CORNELL_C2W, 60.0, 64, 48)
-    img, ref, _ = render_both(renderer, s, 64, 48, 4)
+    img, ref, _ = render_both(renderer, s, 64, 48, 4, schedule=sched)
     compare(img, ref)
-    img, ref, _ = render_both(renderer, s, 64, 48, 4, integrator="direct")
+    img, ref, _ = render_both(renderer, s, 64, 48, 4, integrator="direct", schedule=sched)
     compare(img, ref)
 
 
-def test_c5_smoke_vpt(renderer):
+def test_c5_smoke_vpt(renderer, sched):
     """Config C5 family (synthetic density grid in a BoxMesh + quad light,
     VolumePathTracing(10)) at reduced grid and image size."""
     s = scenes.smoke(48, 36, n=32)
-    img, ref, st = render_both(renderer, s, 48, 36, 4)
+    img, ref, st = render_both(renderer, s, 48, 36, 4, schedule=sched)
     compare(img, ref)
     g = renderer.stats
     assert g.draws == st["draws"] and g.segments == st["segments"] and g.stalled == st["stalled"] == 0
 
 
-def test_vpt_medium_walk_suspends_and_resumes(renderer):
+def test_vpt_medium_walk_suspends_and_resumes(renderer, sched):
     """Many spp per pixel forces delta-tracking walks to cross RNG refills (suspend/resume)."""
     s = scenes.smoke(12, 9, n=32)
-    img, ref, st = render_both(renderer, s, 12, 9, 96)
+    img, ref, st = render_both(renderer, s, 12, 9, 96, schedule=sched)
     compare(img, ref)
     assert renderer.stats.draws == st["draws"]
 

@@ -70,15 +70,17 @@ def test_sphere_scene_c3():
     assert len(light_objs) == 1
 
 
-def test_pinhole_scale():
-    # tan(0.5 * deg2rad(60)) in float (Src/camera.h:45)
-    import ctypes
-    libm = ctypes.CDLL("libm.so.6")
-    libm.tanf.restype, libm.tanf.argtypes = ctypes.c_float, [ctypes.c_float]
+def test_pinhole_scale_is_the_gcc_folded_value():
+    """tan(0.5*deg2rad(FOV)) (Src/camera.h:45): the reference examples pass a constant FOV
+    and GCC -O2 folds the tan correctly rounded (FOV 60 -> 0x1.279a74p-1; glibc's run-time
+    tanf would give 0x1.279a76p-1).  The host layer reproduces the folded value."""
+    import math
     pi = np.float32(3.14159265359)
-    arg = np.float32(0.5) * (np.float32(60.0) / np.float32(180.0) * pi)
-    sc = abi.lib().xrt_pinhole_scale(60.0)
-    assert np.float32(sc) == np.float32(libm.tanf(float(arg)))
+    for fov in (60.0, 45.0, 90.0, 37.5):
+        arg = np.float32(0.5) * (np.float32(fov) / np.float32(180.0) * pi)
+        sc = np.float32(abi.lib().xrt_pinhole_scale(fov))
+        assert sc == np.float32(math.tan(float(arg))), fov
+    assert np.float32(abi.lib().xrt_pinhole_scale(60.0)) == np.float32(float.fromhex("0x1.279a74p-1"))
 
 
 def test_load_obj_missing_file_is_an_error():

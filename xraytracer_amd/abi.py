@@ -14,14 +14,15 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libxrt_hip.so")
 
+XRT_ABI_VERSION = 2   # include/xrt.h XRT_ABI_VERSION
 XRT_OK = 0
 XRT_OBJ_MESH, XRT_OBJ_SPHERE, XRT_OBJ_BOX = 0, 1, 2
 XRT_LIGHT_QUAD, XRT_LIGHT_TRIANGLE, XRT_LIGHT_SPHERE = 0, 1, 2
 XRT_MAT_NONE, XRT_MAT_LAMBERT = 0, 1
 XRT_INTEGRATOR_GI, XRT_INTEGRATOR_DIRECT, XRT_INTEGRATOR_VPT = 0, 1, 2
-XRT_FLAG_TIMING = 1
-XRT_K_SEED, XRT_K_TRACE, XRT_K_SHADE, XRT_K_FINISH, XRT_K_COUNT = 0, 1, 2, 3, 4
-KERNEL_NAMES = ("seed", "trace", "shade", "finish")
+XRT_FLAG_TIMING, XRT_FLAG_WAVEFRONT = 1, 2
+XRT_K_SEED, XRT_K_TRACE, XRT_K_SHADE, XRT_K_FINISH, XRT_K_STEP, XRT_K_COUNT = 0, 1, 2, 3, 4, 5
+KERNEL_NAMES = ("seed", "trace", "shade", "finish", "step")
 
 INTEGRATORS = {"gi": XRT_INTEGRATOR_GI, "direct": XRT_INTEGRATOR_DIRECT, "vpt": XRT_INTEGRATOR_VPT}
 

@@ -12,6 +12,10 @@ hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* 
                         uint32_t blocks, hipStream_t st);
 hipError_t launch_shade(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
                         uint32_t* out_count, uint32_t blocks, hipStream_t st);
+// fused schedule (k_step): LDS bytes it needs for this scene, 0 = scene too large for it
+size_t step_lds_bytes(const KParams& P);
+hipError_t launch_step(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
+                       uint32_t* out_count, uint32_t* zero, uint32_t blocks, hipStream_t st);
 hipError_t launch_finish(const KParams& P, hipStream_t st);
 hipError_t launch_test_rng(const uint32_t* seeds, uint32_t n_seeds, uint32_t skip, uint32_t n, float* out,
                            uint32_t* rings, hipStream_t st);

@@ -47,6 +47,20 @@ struct DObj {
     float pad;
 };
 
+// Mesh object culling record for small triangle scenes: the object's triangle range and
+// an AABB of its vertices grown by a margin far larger than the float error of the
+// Moller-Trumbore test, so skipping an object whose box the ray misses never changes a
+// hit decision.
+struct DObjBox {
+    float bmin[3];
+    int first;
+    float bmax[3];
+    int count_occ;   // triangle count | (occluder << 31)
+};
+constexpr int kSmallTris = 1024;   // scenes up to this size keep every triangle in LDS
+constexpr int kSmallObjs = 256;
+constexpr unsigned kStepLds = 64u * 1024u;   // LDS budget of the fused schedule (k_step)
+
 struct DLight {  // e1/e2/Ng precomputed on the host with the reference constructor's ops
     int kind;
     float v0[3], v1[3], v2[3], e1[3], e2[3], Ng[3], center[3], radius, Le[3];
@@ -77,7 +91,8 @@ struct KParams {
     const DObj* objs;
     const DLight* lights;
     const DSeg* segs;
-    int n_segs, n_lights, n_tris, n_sph, n_box, scene_kind;
+    const DObjBox* obj_box;   // per object, for the small-scene trace path (n_objs entries)
+    int n_segs, n_lights, n_tris, n_sph, n_box, scene_kind, n_objs, small_tri;
     DMedium medium;
     // ---- camera (row-major c2w) + PinholeCamera scale / aspect
     float c2w[16];

@@ -43,11 +43,28 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
     return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
 }
 
+// A slot's stream: ring words x[c], x[c+1], ...  prefetch() issues the loads of the next 8
+// words at once (one memory latency for a whole shade pass instead of one per draw);
+// draws beyond the prefetched words are loaded on demand.
 struct Rng {
     const uint32_t* ring;
     uint32_t c;
+    uint32_t nb = 0;
+    uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0, b4 = 0, b5 = 0, b6 = 0, b7 = 0;
+    __device__ __forceinline__ void prefetch(uint32_t avail) {
+        nb = avail < 8u ? avail : 8u;
+        b0 = ring[c % kRing], b1 = ring[(c + 1) % kRing], b2 = ring[(c + 2) % kRing], b3 = ring[(c + 3) % kRing];
+        b4 = ring[(c + 4) % kRing], b5 = ring[(c + 5) % kRing], b6 = ring[(c + 6) % kRing], b7 = ring[(c + 7) % kRing];
+    }
     __device__ __forceinline__ float next() {
-        const uint32_t y = ring[c % kRing];
+        uint32_t y;
+        if (nb) {
+            y = b0;
+            b0 = b1, b1 = b2, b2 = b3, b3 = b4, b4 = b5, b5 = b6, b6 = b7;
+            --nb;
+        } else {
+            y = ring[c % kRing];
+        }
         ++c;
         return canonical(mt_temper(y));
     }
@@ -327,6 +344,101 @@ __global__ __launch_bounds__(kBlock) void k_trace(KParams P, const uint32_t* __r
     }
 }
 
+// Conservative ray/AABB overlap on [0, tlim] for culling (approximate reciprocal is fine:
+// the boxes carry a margin; fminf/fmaxf drop the NaNs of 0*inf, which only widens the
+// interval).
+__device__ __forceinline__ bool box_overlap(v3 o, v3 inv, const DObjBox& B, float tlim) {
+    const float tx0 = (B.bmin[0] - o.x) * inv.x, tx1 = (B.bmax[0] - o.x) * inv.x;
+    const float ty0 = (B.bmin[1] - o.y) * inv.y, ty1 = (B.bmax[1] - o.y) * inv.y;
+    const float tz0 = (B.bmin[2] - o.z) * inv.z, tz1 = (B.bmax[2] - o.z) * inv.z;
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
+    return !(tn > tf);
+}
+__device__ __forceinline__ v3 rcp3(v3 d) {
+    return mk(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+}
+
+// Small triangle scenes (<= kSmallTris triangles, e.g. the Cornell box): every triangle
+// and the per-object boxes live in LDS for the whole launch; objects are visited in
+// Scene iteration order and a wave skips an object none of its rays can hit (closest-hit
+// rays are culled against the current best t, shadow rays against tmax; area-light
+// objects are never occluders).  Inside an object the triangle order and the strict
+// `t < best` update are the reference's, so results are identical to the linear scan.
+template <int NL>
+__global__ __launch_bounds__(kBlock) void k_trace_small(KParams P, const uint32_t* __restrict__ list,
+                                                        const uint32_t* __restrict__ count, uint32_t* zero_count) {
+    extern __shared__ __attribute__((aligned(16))) f4 lds_small[];
+    f4* ltri = lds_small;
+    DObjBox* lbox = reinterpret_cast<DObjBox*>(lds_small + 3 * P.n_tris);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *zero_count = 0;
+    const int tid = threadIdx.x;
+    for (int q = tid; q < 3 * P.n_tris; q += kBlock) ltri[q] = P.tri[q];
+    for (int q = tid; q < P.n_objs; q += kBlock) lbox[q] = P.obj_box[q];
+    __syncthreads();
+    const uint32_t n = *count;
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const uint32_t i = base + tid;
+        const bool valid = i < n;
+        const uint32_t s = valid ? list[i] : 0;
+        const uint32_t st = valid ? P.state[s] : 0;
+        const bool want = (st & ST_RAY) != 0;
+        const uint32_t smask = (st >> ST_SHADOW_SHIFT) & ((1u << NL) - 1u);
+        v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+        if (want) {
+            o = xyz(P.ray_o[s]);
+            d = xyz(P.ray_d[s]);
+        }
+        v3 so[NL], sd[NL];
+        float stmax[NL];
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+            so[l] = mk(0, 0, 0), sd[l] = mk(0, 0, 0), stmax[l] = 0.0f;
+            if (smask & (1u << l)) {
+                const f4 a = P.sh_o[(size_t)l * P.n_slots + s];
+                so[l] = xyz(a);
+                stmax[l] = a.w;
+                sd[l] = xyz(P.sh_d[(size_t)l * P.n_slots + s]);
+            }
+        }
+        const v3 inv = rcp3(d);
+        uint32_t occ = 0;
+        float best_t = kINF, bu = 0.0f, bv = 0.0f;
+        int best = -1;
+        for (int ob = 0; ob < P.n_objs; ++ob) {
+            const DObjBox B = lbox[ob];
+            const int cnt = B.count_occ & 0x7fffffff;
+            const bool occluder = B.count_occ < 0;
+            const bool ne = want && box_overlap(o, inv, B, best_t);
+            uint32_t nsm = 0;
+            if (occluder) {
+#pragma unroll
+                for (int l = 0; l < NL; ++l)
+                    if ((smask & ~occ & (1u << l)) && box_overlap(so[l], rcp3(sd[l]), B, stmax[l])) nsm |= 1u << l;
+            }
+            if (__ballot(ne || nsm) == 0) continue;
+            for (int k = B.first; k < B.first + cnt; ++k) {
+                const v3 v0 = xyz(ltri[3 * k]), e1 = xyz(ltri[3 * k + 1]), e2 = xyz(ltri[3 * k + 2]);
+                if (ne) {
+                    float t, u, v;
+                    if (ray_tri(o, d, v0, e1, e2, t, u, v) && t < best_t) best_t = t, bu = u, bv = v, best = k;
+                }
+#pragma unroll
+                for (int l = 0; l < NL; ++l) {
+                    if (nsm & ~occ & (1u << l)) {
+                        float t, u, v;
+                        if (ray_tri(so[l], sd[l], v0, e1, e2, t, u, v) && t < stmax[l]) occ |= 1u << l;
+                    }
+                }
+            }
+        }
+        if (valid) {
+            if (want) P.hit[s] = make_float4(best_t, bu, bv, __int_as_float(best));
+            if (smask) P.occ[s] = occ;
+        }
+    }
+}
+
 // =================================================================== shading ====
 struct Surf {
     v3 pos, ng, ns, dpdu, dpdv;
@@ -596,6 +708,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
         uint32_t g = valid ? P.rng_g[s] : 0;
         Rng rng{P.ring + (size_t)s * kRing, valid ? P.rng_c[s] : 0};
         wave_refill(valid && (g - rng.c) < kRngMin, s, g, P.ring, lds_twist[tid >> 6], lane);
+        if (valid) rng.prefetch(g - rng.c);
 
         uint32_t st = valid ? P.state[s] : ST_DONE;
         if (valid) {
@@ -892,6 +1005,404 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
     }
 }
 
+// ============================================================ fused schedule ====
+// k_step: one launch per iteration over the compacted live list; per slot it traces the
+// pending ray, shades the hit (NEE shadow rays are traced immediately, so no shadow state
+// crosses a launch), and finalises/regenerates — the per-pixel sequence of
+// NormalRenderer::doRender + integrate(), one bounce per launch.  The whole scene
+// (triangle geometry and normals' plane, spheres, boxes) lives in LDS, so it is used for
+// scenes up to kStepTris triangles / kStepSph spheres (C1, C2, C3, C5); larger scenes use
+// the multi-pass wavefront (k_shade / k_trace with LDS tiles).
+struct LScene {
+    const f4* tri;      // 3 per triangle
+    const f4* tng;      // geometric normal per triangle
+    const DObjBox* box; // per object (SCN_TRI)
+    const f4* sph;
+    const int* sobj;
+    const f4* bx;       // 2 per box
+};
+
+struct HitRec {
+    float t, u, v;
+    int code;           // winner: (kind << 28) | index, -1 miss
+    int surf, dp;       // mixed scenes: last SurfaceInfo / dpdu writer
+    float st, su, sv, du, dv, t1;
+};
+
+// Scene::intersect over the LDS scene (Src/scene.cpp:190-200)
+template <int SCN>
+__device__ __forceinline__ void closest_l(const KParams& P, const LScene& L, v3 o, v3 d, HitRec& h) {
+    h.t = kINF, h.u = h.v = 0.0f, h.code = -1, h.surf = -1, h.dp = -1, h.t1 = kINF;
+    h.st = h.su = h.sv = h.du = h.dv = 0.0f;
+    if (SCN == SCN_TRI) {
+        const v3 inv = rcp3(d);
+        for (int ob = 0; ob < P.n_objs; ++ob) {
+            const DObjBox B = L.box[ob];
+            if (!box_overlap(o, inv, B, h.t)) continue;
+            const int end = B.first + (B.count_occ & 0x7fffffff);
+            for (int k = B.first; k < end; ++k) {
+                float t, u, v;
+                if (ray_tri(o, d, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t, u, v) &&
+                    t < h.t)
+                    h.t = t, h.u = u, h.v = v, h.code = k;
+            }
+        }
+    } else if (SCN == SCN_SPHERE) {
+        for (int k = 0; k < P.n_sph; ++k) {
+            const f4 S = L.sph[k];
+            float t;
+            if (sphere_hit(o, d, xyz(S), S.w, t) && t < h.t) h.t = t, h.code = (1 << 28) | k;
+        }
+    } else {
+        for (int sg = 0; sg < P.n_segs; ++sg) {
+            const DSeg seg = P.segs[sg];
+            if (seg.kind == SEG_TRI) {
+                for (int k = seg.first; k < seg.first + seg.count; ++k) {
+                    float t, u, v;
+                    if (ray_tri(o, d, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t, u, v) &&
+                        t < h.t)
+                        h.t = t, h.u = u, h.v = v, h.code = k, h.surf = k, h.st = t, h.su = u, h.sv = v, h.dp = k,
+                        h.du = u, h.dv = v;
+                }
+            } else if (seg.kind == SEG_SPHERE) {
+                for (int k = seg.first; k < seg.first + seg.count; ++k) {
+                    const f4 S = L.sph[k];
+                    float t;
+                    if (sphere_hit(o, d, xyz(S), S.w, t) && t < h.t)
+                        h.t = t, h.u = h.v = 0.0f, h.code = (1 << 28) | k, h.surf = h.code, h.st = t;
+                }
+            } else {
+                for (int b = seg.first; b < seg.first + seg.count; ++b) {
+                    float t0, t1;
+                    if (box_hit(o, d, xyz(L.bx[2 * b]), xyz(L.bx[2 * b + 1]), t0, t1))
+                        h.t = t0, h.t1 = t1, h.code = (2 << 28) | b;
+                }
+            }
+        }
+    }
+}
+
+// Scene::occluded over the LDS scene (Src/scene.cpp:202-211): area-light objects skipped
+template <int SCN>
+__device__ __forceinline__ bool occluded_l(const KParams& P, const LScene& L, v3 o, v3 d, float tmax) {
+    if (SCN == SCN_TRI) {
+        const v3 inv = rcp3(d);
+        for (int ob = 0; ob < P.n_objs; ++ob) {
+            const DObjBox B = L.box[ob];
+            if (B.count_occ >= 0 || !box_overlap(o, inv, B, tmax)) continue;
+            const int end = B.first + (B.count_occ & 0x7fffffff);
+            for (int k = B.first; k < end; ++k) {
+                float t, u, v;
+                if (ray_tri(o, d, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t, u, v) &&
+                    t < tmax)
+                    return true;
+            }
+        }
+        return false;
+    } else {
+        for (int sg = 0; sg < P.n_segs; ++sg) {
+            const DSeg seg = P.segs[sg];
+            if (SCN == SCN_MIXED && seg.kind == SEG_TRI) {
+                for (int k = seg.first; k < seg.first + seg.count; ++k) {
+                    if (L.tri[3 * k + 1].w == 0.0f) continue;
+                    float t, u, v;
+                    if (ray_tri(o, d, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t, u, v) &&
+                        t < tmax)
+                        return true;
+                }
+            } else if (seg.kind == SEG_SPHERE) {
+                for (int k = seg.first; k < seg.first + seg.count; ++k) {
+                    if (!(L.sobj[k] & (1 << 30))) continue;
+                    const f4 S = L.sph[k];
+                    float t;
+                    if (sphere_hit(o, d, xyz(S), S.w, t) && t < tmax) return true;
+                }
+            } else if (SCN == SCN_MIXED && seg.kind == SEG_BOX) {
+                return true;   // BoxMesh::occluded (Src/primitive.h:266-268)
+            }
+        }
+        return false;
+    }
+}
+
+// IntersectInfo::surfaceInfo from a hit record (see surface<>)
+template <int SCN>
+__device__ __forceinline__ int surface_l(const KParams& P, const LScene& L, v3 o, v3 d, const HitRec& h, Surf& S) {
+    S.pos = S.ng = S.ns = S.dpdu = S.dpdv = mk(0, 0, 0);
+    if (h.code < 0) return -1;
+    int surf = h.code, dp = (SCN == SCN_TRI) ? h.code : -1;
+    float st = h.t, su = h.u, sv = h.v, du = h.u, dv = h.v;
+    if (SCN == SCN_MIXED) surf = h.surf, dp = h.dp, st = h.st, su = h.su, sv = h.sv, du = h.du, dv = h.dv;
+    if (surf >= 0) {
+        const int kind = surf >> 28, idx = surf & 0x0fffffff;
+        S.pos = ray_at(o, d, st);
+        if (kind == SEG_TRI) {
+            S.ng = xyz(L.tng[idx]);
+            S.ns = tri_ns(P, idx, su, sv);
+        } else {
+            S.ng = normalize(ray_at(o, d, st) - xyz(L.sph[idx]));
+            S.ns = S.ng;
+        }
+    }
+    if (dp >= 0) onb(tri_ns(P, dp & 0x0fffffff, du, dv), S.dpdu, S.dpdv);
+    const int kind = h.code >> 28, idx = h.code & 0x0fffffff;
+    if (kind == SEG_TRI) return __float_as_int(L.tri[3 * idx].w);
+    if (kind == SEG_SPHERE) return L.sobj[idx] & 0x3fffffff;
+    return __float_as_int(L.bx[2 * idx].w);
+}
+
+template <int SCN, int INTEG>
+__global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __restrict__ list,
+                                                  const uint32_t* __restrict__ count, uint32_t* __restrict__ out,
+                                                  uint32_t* out_count, uint32_t* zero_count) {
+    extern __shared__ __attribute__((aligned(16))) f4 lds_step[];
+    // carve: twist scratch | tri | tng | boxes | spheres | sphere objects | medium boxes
+    uint32_t* lds_twist = reinterpret_cast<uint32_t*>(lds_step);
+    f4* p = lds_step + (kBlock / 64) * 2 * kMT / 4;
+    LScene L;
+    L.tri = p;
+    p += 3 * P.n_tris;
+    L.tng = p;
+    p += P.n_tris;
+    L.box = reinterpret_cast<const DObjBox*>(p);
+    p += (SCN == SCN_TRI ? 2 * P.n_objs : 0);
+    L.sph = p;
+    p += P.n_sph;
+    L.bx = p;
+    p += 2 * P.n_box;
+    L.sobj = reinterpret_cast<const int*>(p);
+    const int tid = threadIdx.x, lane = tid & 63;
+    {
+        f4* w = const_cast<f4*>(L.tri);
+        for (int q = tid; q < 3 * P.n_tris; q += kBlock) w[q] = P.tri[q];
+        w = const_cast<f4*>(L.tng);
+        for (int q = tid; q < P.n_tris; q += kBlock) w[q] = P.tri_ng[q];
+        if (SCN == SCN_TRI) {
+            DObjBox* wb = const_cast<DObjBox*>(L.box);
+            for (int q = tid; q < P.n_objs; q += kBlock) wb[q] = P.obj_box[q];
+        }
+        w = const_cast<f4*>(L.sph);
+        for (int q = tid; q < P.n_sph; q += kBlock) w[q] = P.sph[q];
+        int* wo = const_cast<int*>(L.sobj);
+        for (int q = tid; q < P.n_sph; q += kBlock) wo[q] = P.sph_obj[q];
+        w = const_cast<f4*>(L.bx);
+        for (int q = tid; q < 2 * P.n_box; q += kBlock) w[q] = P.box[q];
+    }
+    if (blockIdx.x == 0 && tid == 0) *zero_count = 0;
+    __syncthreads();
+    const uint32_t n = *count;
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const uint32_t i = base + tid;
+        const bool valid = i < n;
+        const uint32_t s = valid ? list[i] : 0;
+        uint32_t g = valid ? P.rng_g[s] : 0;
+        Rng rng{P.ring + (size_t)s * kRing, valid ? P.rng_c[s] : 0};
+        wave_refill(valid && (g - rng.c) < kRngMin, s, g, P.ring, lds_twist + (tid >> 6) * 2 * kMT, lane);
+        uint32_t st = valid ? P.state[s] : ST_DONE;
+        if (valid) {
+            rng.prefetch(g - rng.c);
+            uint32_t depth = P.depth[s];
+            uint32_t k = P.sample_k[s];
+            v3 thr = mk(1, 1, 1), rad = mk(0, 0, 0), o, d;
+            uint32_t nseg = 0, nsh = 0, nrej = 0, nstall = 0;
+            const uint32_t col = s % P.width, row = P.shard_index + P.shard_count * (s / P.width);
+            bool ended = false, trace = false;
+            if (st & ST_REGEN) {
+                // next sample: jitter draws + camera ray (Src/renderer.cpp:44-50)
+                st &= ~ST_REGEN;
+                const float u = ((float)(int)col + rng.next()) / (float)P.width;
+                const float v = ((float)(int)row + rng.next()) / (float)P.height;
+                camera_ray(P, u, v, o, d);
+                depth = 0;
+                if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) ended = true;
+                else trace = true;
+            } else {
+                thr = xyz(P.thr[s]), rad = xyz(P.rad[s]);
+                o = xyz(P.ray_o[s]), d = xyz(P.ray_d[s]);
+                trace = !(st & ST_MEDIUM);
+            }
+            bool walk = false;
+            float mt = 0.0f, mt1 = 0.0f;
+            v3 tt = mk(1, 1, 1), sa = mk(0, 0, 0);
+            if (INTEG == XRT_INTEGRATOR_VPT && (st & ST_MEDIUM)) {
+                st &= ~ST_MEDIUM;
+                const f4 m1 = P.med[s], m2 = P.med2[s];
+                mt = m1.x, mt1 = m1.y, sa = mk(m1.z, m1.w, m2.w), tt = xyz(m2);
+                walk = true;
+            }
+            if (trace) {
+                ++nseg;
+                HitRec h;
+                closest_l<SCN>(P, L, o, d, h);
+                Surf S;
+                const int obj = surface_l<SCN>(P, L, o, d, h, S);
+                if (INTEG == XRT_INTEGRATOR_DIRECT) {
+                    // DirectIntegrator::integrate (Src/integrator.h:82-119)
+                    if (obj < 0) {
+                        rad = mk((float)0.18, (float)0.18, (float)0.18);
+                    } else if (P.objs[obj].light >= 0) {
+                        rad = light_Le(P.lights[P.objs[obj].light], S.ns, d);
+                    } else {
+                        const DObj ob = P.objs[obj];
+                        for (int l = 0; l < P.n_lights; ++l) {
+                            v3 wi = mk(0, 0, 0);
+                            float tmax = 0.0f, pdf = 0.0f;
+                            const v3 Lv = light_sample(P.lights[l], S.pos, wi, pdf, tmax, rng);
+                            if (pdf == 0.0f) continue;
+                            const float bias = 0.01f;
+                            ++nsh;
+                            const bool vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias);
+                            const float cosv = smax(0.0f, dot(S.ng, wi));
+                            const v3 fr = eval_bxdf(ob);
+                            rad = rad + (((fr * (float)vis) * Lv) * cosv) / pdf;
+                        }
+                    }
+                    ended = true;
+                } else if (INTEG == XRT_INTEGRATOR_VPT) {
+                    // VolumePathTracing::integrate loop body (Src/integrator.h:418-469)
+                    if (obj < 0) {
+                        rad = rad + (thr * mk(0.0f, 0.0f, 0.0f)) * (float)(depth != 0);
+                        ended = true;
+                    } else {
+                        bool alive = true;
+                        if (depth > 0) {
+                            const float pr = smin((thr.x + thr.y + thr.z) / 3.0f, 1.0f);
+                            if (rng.next() >= pr) alive = false, ended = true;
+                            else thr = thr / mk(pr, pr, pr);
+                        }
+                        const DObj ob = P.objs[obj];
+                        if (alive && ob.light >= 0) {
+                            rad = rad + thr * light_Le(P.lights[ob.light], S.ns, d);
+                            alive = false, ended = true;
+                        }
+                        if (alive) {
+                            if (ob.medium >= 0) {
+                                mt = h.t, mt1 = h.t1;
+                                sa = ld3(P.medium.absorption) * medium_density(P.medium, ray_at(o, d, mt));
+                                walk = true;
+                            } else {
+                                ++nstall;
+                                ended = true;
+                            }
+                        }
+                    }
+                } else {
+                    // GIIntegrator::integrate loop body (Src/integrator.h:214-284)
+                    if (obj < 0) {
+                        rad = rad + thr * mk(0.0f, 0.0f, 0.0f);
+                        ended = true;
+                    } else {
+                        bool alive = true;
+                        if (depth > 0) {
+                            const float pr = smin((thr.x + thr.y + thr.z) / 3.0f, 1.0f);
+                            if (rng.next() >= pr) alive = false, ended = true;
+                            else thr = thr / mk(pr, pr, pr);
+                        }
+                        const DObj ob = P.objs[obj];
+                        if (alive && ob.light >= 0) {
+                            if (depth == 0) rad = rad + thr * light_Le(P.lights[ob.light], S.ns, d);
+                            alive = false, ended = true;
+                        }
+                        if (alive) {
+                            v3 directL = mk(0, 0, 0);
+                            for (int l = 0; l < P.n_lights; ++l) {
+                                v3 L_light = mk(0, 0, 0);
+                                v3 wi = mk(0, 0, 0);
+                                float tmax = 0.0f, pdf = 0.0f;
+                                const v3 Lv = light_sample(P.lights[l], S.pos, wi, pdf, tmax, rng);
+                                if (pdf == 0.0f) continue;
+                                const float bias = 0.01f;
+                                ++nsh;
+                                const bool vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias);
+                                const float cosv = smax(0.0f, dot(S.ng, wi));
+                                const v3 fr = eval_bxdf(ob);
+                                L_light = L_light + (((fr * (float)vis) * Lv) * cosv) / pdf;
+                                directL = directL + L_light;
+                            }
+                            rad = rad + thr * directL;
+                            float pdf = 1.0f;
+                            v3 nd = mk(0, 0, 0), fr = mk(0, 0, 0);
+                            if (ob.material == 1) {
+                                nd = lambert_sample(S, rng);
+                                pdf = 1.0f / (2.0f * kPI);
+                                fr = eval_bxdf(ob);
+                            }
+                            const float cosv = smax(0.0f, dot(nd, S.ng));
+                            thr = thr * ((fr * cosv) / pdf);
+                            o = S.pos + S.ng * 0.01f;
+                            d = nd;
+                            ++depth;
+                            if (depth >= P.max_depth) ended = true;
+                        }
+                    }
+                }
+            }
+            if (INTEG == XRT_INTEGRATOR_VPT && walk) {
+                v3 pos, dir, tm;
+                const int r = delta_track(P, o, d, thr, mt, mt1, tt, sa, rng, g, pos, dir, tm);
+                if (r == 2) {
+                    st |= ST_MEDIUM;
+                    P.med[s] = make_float4(mt, mt1, sa.x, sa.y);
+                    P.med2[s] = make_float4(tt.x, tt.y, tt.z, sa.z);
+                } else {
+                    o = pos, d = dir;
+                    thr = thr * tm;
+                    if (r == 1) ++depth;
+                    if (depth >= P.max_depth) ended = true;
+                }
+            }
+            // finish the sample (Src/renderer.cpp:55-75); the next one starts next launch
+            while (ended) {
+                ended = false;
+                const v3 r = rad / 1.0f;
+                if (__builtin_isnan(r.x) || __builtin_isnan(r.y) || __builtin_isnan(r.z) || __builtin_isinf(r.x) ||
+                    __builtin_isinf(r.y) || __builtin_isinf(r.z) || r.x < 0.0f || r.y < 0.0f || r.z < 0.0f) {
+                    ++nrej;
+                } else {
+                    float* px = P.fb + 3 * ((size_t)col + (size_t)P.width * row);
+                    px[0] = px[0] + r.x, px[1] = px[1] + r.y, px[2] = px[2] + r.z;
+                }
+                ++k;
+                if (k >= P.spp) {
+                    st = ST_DONE;
+                } else if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) {
+                    (void)rng.next(), (void)rng.next();   // the next sample's jitter; radiance 0
+                    rad = mk(0, 0, 0);
+                    ended = true;
+                } else {
+                    st |= ST_REGEN;
+                }
+            }
+            P.state[s] = st;
+            if (!(st & (ST_DONE | ST_REGEN))) {
+                P.depth[s] = depth;
+                P.thr[s] = pk(thr);
+                P.rad[s] = pk(rad);
+                P.ray_o[s] = pk(o);
+                P.ray_d[s] = pk(d);
+            }
+            P.sample_k[s] = k;
+            P.rng_c[s] = rng.c;
+            P.rng_g[s] = g;
+            if (nseg) P.c_seg[s] += nseg;
+            if (nsh) P.c_shadow[s] += nsh;
+            if (nrej) P.c_rej[s] += nrej;
+            if (nstall) P.c_stall[s] += nstall;
+        }
+        const bool keep = valid && !(st & ST_DONE);
+        const uint64_t m = __ballot(keep);
+        if (m) {
+            const uint32_t cnt = __popcll(m);
+            const uint32_t pre = __popcll(m & ((1ull << lane) - 1ull));
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            uint32_t wbase = 0;
+            if (lane == leader) wbase = atomicAdd(out_count, cnt);
+            wbase = __shfl(wbase, leader);
+            if (keep) out[wbase + pre] = s;
+        }
+    }
+}
+
 // ================================================================== k_finish ====
 // Image::operator/=(Vec3f(n_samples)) over this shard's pixels + counter reduction.
 __global__ __launch_bounds__(kBlock) void k_finish(KParams P) {
@@ -1013,6 +1524,15 @@ static hipError_t trace_nl(const KParams& P, const uint32_t* list, const uint32_
 
 hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
                         uint32_t blocks, hipStream_t st) {
+    if (P.small_tri) {
+        const size_t lds = (size_t)P.n_tris * 3 * sizeof(f4) + (size_t)P.n_objs * sizeof(DObjBox);
+        if (P.n_lights <= 1)
+            hipLaunchKernelGGL((k_trace_small<1>), dim3(blocks), dim3(kBlock), lds, st, P, list, count, zero);
+        else
+            hipLaunchKernelGGL((k_trace_small<kMaxLights>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
+                               zero);
+        return hipGetLastError();
+    }
     switch (P.scene_kind) {
         case SCN_TRI: return trace_nl<SCN_TRI>(P, list, count, zero, blocks, st);
         case SCN_SPHERE: return trace_nl<SCN_SPHERE>(P, list, count, zero, blocks, st);
@@ -1041,6 +1561,42 @@ hipError_t launch_shade(const KParams& P, const uint32_t* list, const uint32_t* 
         case SCN_TRI: return shade_i<SCN_TRI>(P, list, count, out, out_count, blocks, st);
         case SCN_SPHERE: return shade_i<SCN_SPHERE>(P, list, count, out, out_count, blocks, st);
         default: return shade_i<SCN_MIXED>(P, list, count, out, out_count, blocks, st);
+    }
+}
+
+size_t step_lds_bytes(const KParams& P) {
+    if (P.scene_kind == SCN_TRI && !P.small_tri) return 0;   // needs the per-object boxes
+    const size_t twist = (kBlock / 64) * 2 * kMT * sizeof(uint32_t);
+    const size_t scene = sizeof(f4) * (4 * (size_t)P.n_tris + (P.scene_kind == SCN_TRI ? 2 * (size_t)P.n_objs : 0) +
+                                       (size_t)P.n_sph + 2 * (size_t)P.n_box) +
+                         sizeof(int) * (size_t)P.n_sph;
+    const size_t total = twist + scene;
+    return total <= kStepLds ? total : 0;
+}
+
+template <int SCN>
+static hipError_t step_i(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
+                         uint32_t* out_count, uint32_t* zero, uint32_t blocks, hipStream_t st) {
+    const size_t lds = step_lds_bytes(P);
+    if (P.integrator == XRT_INTEGRATOR_DIRECT)
+        hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_DIRECT>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
+                           out, out_count, zero);
+    else if (P.integrator == XRT_INTEGRATOR_VPT)
+        hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_VPT>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
+                           out, out_count, zero);
+    else
+        hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_GI>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
+                           out, out_count, zero);
+    return hipGetLastError();
+}
+
+hipError_t launch_step(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
+                       uint32_t* out_count, uint32_t* zero, uint32_t blocks, hipStream_t st) {
+    if (!step_lds_bytes(P)) return hipErrorInvalidValue;
+    switch (P.scene_kind) {
+        case SCN_TRI: return step_i<SCN_TRI>(P, list, count, out, out_count, zero, blocks, st);
+        case SCN_SPHERE: return step_i<SCN_SPHERE>(P, list, count, out, out_count, zero, blocks, st);
+        default: return step_i<SCN_MIXED>(P, list, count, out, out_count, zero, blocks, st);
     }
 }
 

@@ -33,7 +33,7 @@ struct xrt_ctx {
     std::string err;
     // scene
     std::vector<DevBuf*> scene_bufs;
-    DevBuf tri, tri_ng, tri_nrm, sph, sph_obj, box, objs, lights, segs, density;
+    DevBuf tri, tri_ng, tri_nrm, sph, sph_obj, box, objs, lights, segs, density, obj_box;
     KParams base{};
     bool has_scene = false, has_camera = false, has_medium = false;
     // slots
@@ -124,7 +124,7 @@ void xrt_destroy(xrt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->tri, &c->tri_ng, &c->tri_nrm, &c->sph, &c->sph_obj, &c->box, &c->objs, &c->lights,
-                     &c->segs, &c->density, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
+                     &c->segs, &c->density, &c->obj_box, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
                      &c->hit2, &c->hit3, &c->sh_o, &c->sh_d, &c->sh_c, &c->med, &c->med2, &c->state,
                      &c->sample_k, &c->depth, &c->occ, &c->rng_c, &c->rng_g, &c->ring, &c->c_seg, &c->c_shadow,
                      &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch};
@@ -245,6 +245,40 @@ int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
     bool only_tri = true, only_sph = true;
     for (const DSeg& g : segs) only_tri &= g.kind == SEG_TRI, only_sph &= g.kind == SEG_SPHERE;
     P.scene_kind = (only_tri || segs.empty()) ? SCN_TRI : (only_sph ? SCN_SPHERE : SCN_MIXED);
+    // small triangle scenes: per-object culling boxes for k_trace_small.  Margin: 1e-3 of
+    // the scene diagonal + 1e-3, orders of magnitude above the float error of a
+    // Moller-Trumbore hit position, so culling never removes a hit the linear scan accepts.
+    P.small_tri = 0;
+    P.n_objs = (int)objs.size();
+    if (P.scene_kind == SCN_TRI && P.n_tris <= kSmallTris && P.n_objs <= kSmallObjs && P.n_tris > 0) {
+        float lo[3] = {3e38f, 3e38f, 3e38f}, hi[3] = {-3e38f, -3e38f, -3e38f};
+        std::vector<DObjBox> boxes(objs.size());
+        int tri_first = 0;
+        for (size_t k = 0; k < objs.size(); ++k) {
+            DObjBox& b = boxes[k];
+            const int cnt = s->objects[k].count;
+            b.first = tri_first;
+            b.count_occ = cnt | (objs[k].light < 0 ? (int)0x80000000 : 0);
+            for (int q = 0; q < 3; ++q) b.bmin[q] = 3e38f, b.bmax[q] = -3e38f;
+            for (int t = tri_first; t < tri_first + cnt; ++t) {
+                const f4 v0 = tri[3 * t], e1 = tri[3 * t + 1], e2 = tri[3 * t + 2];
+                const float vs[3][3] = {{v0.x, v0.y, v0.z}, {v0.x + e1.x, v0.y + e1.y, v0.z + e1.z},
+                                        {v0.x + e2.x, v0.y + e2.y, v0.z + e2.z}};
+                for (int a = 0; a < 3; ++a)
+                    for (int q = 0; q < 3; ++q) b.bmin[q] = std::min(b.bmin[q], vs[a][q]), b.bmax[q] = std::max(b.bmax[q], vs[a][q]);
+            }
+            for (int q = 0; q < 3; ++q) lo[q] = std::min(lo[q], b.bmin[q]), hi[q] = std::max(hi[q], b.bmax[q]);
+            tri_first += cnt;
+        }
+        const float diag = std::sqrt((hi[0] - lo[0]) * (hi[0] - lo[0]) + (hi[1] - lo[1]) * (hi[1] - lo[1]) +
+                                     (hi[2] - lo[2]) * (hi[2] - lo[2]));
+        const float margin = 1e-3f * diag + 1e-3f;
+        for (DObjBox& b : boxes)
+            for (int q = 0; q < 3; ++q) b.bmin[q] -= margin, b.bmax[q] += margin;
+        if ((rc = upload(c, c->obj_box, boxes.data(), boxes.size() * sizeof(DObjBox)))) return rc;
+        P.obj_box = as<DObjBox>(c->obj_box);
+        P.small_tri = 1;
+    }
     c->has_scene = true;
     return XRT_OK;
 }
@@ -391,20 +425,40 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     uint64_t it = 0;
     int poll_slot = 0;
     bool done = false;
+    // Schedule: the fused k_step (scene resident in LDS, one launch per bounce) when the
+    // scene fits, else the multi-pass wavefront (k_shade, then k_trace streaming the scene
+    // through LDS tiles).  k_step rotates three live counters: launch i reads counts[i%3],
+    // appends to counts[(i+1)%3] and clears counts[(i+2)%3] for launch i+1.
+    const bool fused = !(p->flags & XRT_FLAG_WAVEFRONT) && step_lds_bytes(P) != 0;
     for (; it < cap_iters && !done; ++it) {
         const int cur = (int)(it & 1), nxt = cur ^ 1;
-        hipError_t e = launch(XRT_K_SHADE, [&] {
-            return launch_shade(P, lists[cur], counts + cur, lists[nxt], counts + nxt, blocks, c->stream);
-        });
-        if (e != hipSuccess) return hip_err(c, e, "k_shade");
+        uint32_t* live = nullptr;
+        if (fused) {
+            const int ci = (int)(it % 3), co = (int)((it + 1) % 3), cz = (int)((it + 2) % 3);
+            live = counts + co;
+            hipError_t e = launch(XRT_K_STEP, [&] {
+                return launch_step(P, lists[cur], counts + ci, lists[nxt], counts + co, counts + cz, blocks, c->stream);
+            });
+            if (e != hipSuccess) return hip_err(c, e, "k_step");
+        } else {
+            live = counts + nxt;
+            hipError_t e = launch(XRT_K_SHADE, [&] {
+                return launch_shade(P, lists[cur], counts + cur, lists[nxt], counts + nxt, blocks, c->stream);
+            });
+            if (e != hipSuccess) return hip_err(c, e, "k_shade");
+        }
         if (it % kPoll == kPoll - 1) {
             const int ps = poll_slot++ % 8;
-            HIPCHK(c, hipMemcpyAsync(c->h_poll + ps, counts + nxt, 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipMemcpyAsync(c->h_poll + ps, live, 4, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(c, hipEventRecord(poll_ev[ps], c->stream));
             polls.push_back({it, poll_ev[ps], ps});
         }
-        e = launch(XRT_K_TRACE, [&] { return launch_trace(P, lists[nxt], counts + nxt, counts + cur, blocks, c->stream); });
-        if (e != hipSuccess) return hip_err(c, e, "k_trace");
+        if (!fused) {
+            hipError_t e = launch(XRT_K_TRACE, [&] {
+                return launch_trace(P, lists[nxt], counts + nxt, counts + cur, blocks, c->stream);
+            });
+            if (e != hipSuccess) return hip_err(c, e, "k_trace");
+        }
         // retire polls: non-blocking when possible, blocking when too far ahead
         while (!polls.empty()) {
             Poll& q = polls.front();
@@ -423,7 +477,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     if (!done) {
         // the iteration cap was reached without observing an empty list: verify
         uint32_t left = 0;
-        HIPCHK(c, hipMemcpy(&left, counts + (it & 1), 4, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(&left, counts + (fused ? it % 3 : it & 1), 4, hipMemcpyDeviceToHost));
         if (left != 0) return set_err(c, XRT_ERR_HIP, "iteration cap reached with live paths");
     }
     unsigned long long hs[8] = {0};
