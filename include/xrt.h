@@ -119,7 +119,10 @@ typedef struct {
     uint32_t flags;          /* XRT_FLAG_*                                              */
 } xrt_render_params;
 
-enum { XRT_K_SEED = 0, XRT_K_TRACE = 1, XRT_K_SHADE = 2, XRT_K_FINISH = 3, XRT_K_STEP = 4, XRT_K_COUNT = 5 };
+enum {
+    XRT_K_SEED = 0, XRT_K_TRACE = 1, XRT_K_SHADE = 2, XRT_K_FINISH = 3, XRT_K_STEP = 4, XRT_K_REFILL = 5,
+    XRT_K_COUNT = 6
+};
 
 typedef struct {
     double wall_ms;              /* host wall clock of the render call (upload excluded) */
@@ -130,7 +133,7 @@ typedef struct {
     uint64_t shadow_rays;        /* Scene::occluded calls                                  */
     uint64_t draws;              /* RNG draws (Sampler::getNext1D)                         */
     uint64_t rejected;           /* samples dropped by the NaN/Inf/negative check          */
-    uint64_t iterations;         /* trace+shade pass pairs, or k_step launches             */
+    uint64_t iterations;         /* trace+shade pass pairs, or k_step rounds               */
     uint64_t path_slots;         /* slots in flight (pixels of this shard)                 */
     uint64_t trace_slot_visits;  /* sum over trace launches of active slots                */
     uint64_t stalled;            /* paths stopped by the VPT no-progress guard             */

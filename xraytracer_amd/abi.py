@@ -21,8 +21,8 @@ XRT_LIGHT_QUAD, XRT_LIGHT_TRIANGLE, XRT_LIGHT_SPHERE = 0, 1, 2
 XRT_MAT_NONE, XRT_MAT_LAMBERT = 0, 1
 XRT_INTEGRATOR_GI, XRT_INTEGRATOR_DIRECT, XRT_INTEGRATOR_VPT = 0, 1, 2
 XRT_FLAG_TIMING, XRT_FLAG_WAVEFRONT = 1, 2
-XRT_K_SEED, XRT_K_TRACE, XRT_K_SHADE, XRT_K_FINISH, XRT_K_STEP, XRT_K_COUNT = 0, 1, 2, 3, 4, 5
-KERNEL_NAMES = ("seed", "trace", "shade", "finish", "step")
+XRT_K_SEED, XRT_K_TRACE, XRT_K_SHADE, XRT_K_FINISH, XRT_K_STEP, XRT_K_REFILL, XRT_K_COUNT = 0, 1, 2, 3, 4, 5, 6
+KERNEL_NAMES = ("seed", "trace", "shade", "finish", "step", "refill")
 
 INTEGRATORS = {"gi": XRT_INTEGRATOR_GI, "direct": XRT_INTEGRATOR_DIRECT, "vpt": XRT_INTEGRATOR_VPT}
 

@@ -7,15 +7,21 @@
 #include "wavefront.h"
 
 namespace xrt {
-hipError_t launch_seed(const KParams& P, uint32_t* list, uint32_t* count, uint32_t* count_other, hipStream_t st);
+hipError_t launch_seed(const KParams& P, uint32_t* list, uint32_t* count, uint32_t* count_other,
+                       uint32_t* req_count, hipStream_t st);
+// twist the rings of the slots on P.req (count at *count); clears *zero_count
+hipError_t launch_refill(const KParams& P, const uint32_t* count, uint32_t* zero_count, hipStream_t st);
 hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
                         uint32_t blocks, hipStream_t st);
 hipError_t launch_shade(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
-                        uint32_t* out_count, uint32_t blocks, hipStream_t st);
+                        uint32_t* out_count, uint32_t* req_count, uint32_t blocks, hipStream_t st);
 // fused schedule (k_step): LDS bytes it needs for this scene, 0 = scene too large for it
 size_t step_lds_bytes(const KParams& P);
+// up to `visits` path segments per live slot; appends survivors to out (partitioned
+// counters out_count), low-RNG slots to P.req (req_count); clears zero (next-next round)
 hipError_t launch_step(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
-                       uint32_t* out_count, uint32_t* zero, uint32_t blocks, hipStream_t st);
+                       uint32_t* out_count, uint32_t* zero, uint32_t* req_count, uint32_t visits, uint32_t blocks,
+                       hipStream_t st);
 hipError_t launch_finish(const KParams& P, hipStream_t st);
 hipError_t launch_test_rng(const uint32_t* seeds, uint32_t n_seeds, uint32_t skip, uint32_t n, float* out,
                            uint32_t* rings, hipStream_t st);

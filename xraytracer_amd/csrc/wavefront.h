@@ -8,7 +8,9 @@
 //   slots  : one path slot per pixel of this shard; all per-slot state is SoA (float4 /
 //            uint32 arrays indexed by slot) so a wave's loads are coalesced.
 //   RNG    : per slot a 1248-word ring (two 624-word mt19937 blocks) + cursor/generated
-//            counters; refilled one 624-word twist at a time by a whole wave.
+//            counters.  A shading visit that finds fewer than kRngMin words left puts the
+//            slot on a refill list; k_refill (every kRefillEvery launches) twists each
+//            listed ring with one whole wave, all listed slots in parallel.
 #pragma once
 #include <stdint.h>
 
@@ -21,7 +23,17 @@ namespace xrt {
 constexpr int kMaxLights = 4;        // shadow rays in flight per slot (one per area light)
 constexpr uint32_t kMT = 624;        // mt19937 state words
 constexpr uint32_t kRing = 1248;     // ring words per slot
-constexpr uint32_t kRngMin = 64;     // refill when fewer draws than this remain
+constexpr uint32_t kRngMin = 64;     // request a refill when fewer words than this remain
+constexpr uint32_t kRngVisit = 16;   // a slot visit needs at least this many (max draws of a
+                                     // GI/Direct visit with kMaxLights lights is 13; VPT walks
+                                     // suspend themselves below 8)
+constexpr uint32_t kMaxParts = 64;   // live-list partitions (counters per list)
+constexpr uint32_t kRefillEvery = 4; // wavefront schedule: k_refill after every 4th k_shade
+constexpr uint32_t kStepVisits = 4;  // fused schedule: path segments per slot per k_step
+constexpr uint32_t kStepRefill = 2;  // fused schedule: k_refill after every 2nd k_step
+constexpr uint32_t kRngKeep = 128;   // fused schedule: a slot queues a refill below this
+                                     // (>= kStepRefill * kStepVisits * 13 + kRngVisit: a
+                                     // GI/Direct slot never waits for words)
 
 // slot state bits
 enum : uint32_t {
@@ -31,6 +43,7 @@ enum : uint32_t {
     ST_REGEN = 8u,    // slot must start its next sample
     ST_DONE = 16u,    // all samples of this pixel are done
     ST_MEDIUM = 32u,  // VPT delta-tracking loop suspended (resumes after an RNG refill)
+    ST_RNGREQ = 64u,  // slot is on the refill list (k_refill twists its ring and clears this)
     ST_SHADOW_SHIFT = 8u  // bits 8..15: which lights have a shadow ray in flight
 };
 
@@ -100,6 +113,7 @@ struct KParams {
     // ---- render
     int integrator;
     uint32_t max_depth, width, height, spp, shard_index, shard_count, n_slots;
+    uint32_t n_part, part_cap;   // live-list partitions: n_part (<= kMaxParts) of part_cap slots
     // ---- slot state (SoA)
     f4 *ray_o, *ray_d, *thr, *rad, *thr_prev;
     f4 *hit;     // t, u, v, code(bits)        code: -1 miss, (kind << 28) | prim
@@ -112,6 +126,7 @@ struct KParams {
     f4 *med2;
     uint32_t *state, *sample_k, *depth, *occ;
     uint32_t *rng_c, *rng_g, *ring;
+    uint32_t *req;             // refill request list (slots)
     uint32_t *c_seg, *c_shadow, *c_rej, *c_stall;
     float* fb;                 // [height][width][3]
     unsigned long long* stats; // device reduction target: seg, shadow, draws, rej, stall

@@ -77,29 +77,42 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // One mt19937 twist of a slot's stream done by a whole wave: x[g+k] = x[g+k-227] ^
-// mix(x[g+k-624], x[g+k-623]) for k = 0..623 (libstdc++ _M_gen_rand), computed in three
-// dependency-free chunks of 227/227/170 words through LDS; the new block lands in ring
-// half g % 1248 over the oldest (fully consumed) block.
-__device__ void wave_twist(uint32_t* ring, uint32_t g, uint32_t* lds, int lane) {
+// mix(x[g+k-624], x[g+k-623]) for k = 0..623 (libstdc++ _M_gen_rand).  Split into the
+// chunks k = m, 227 + m, 454 + m (m = lane + 64 j), the word each chunk needs from the
+// previous one, x[g+k-227], is the same lane's register — no LDS, no barrier.  The new
+// block lands in ring half g % 1248, over the oldest (fully consumed) block.  Must be
+// called by every lane of the wave.
+__device__ void wave_twist(uint32_t* ring, uint32_t g, int lane) {
     const uint32_t h = g % kRing;
-    const uint32_t hp = kMT - h;
-    uint32_t* old = lds;
-    uint32_t* nw = lds + kMT;
-    for (uint32_t i = lane; i < kMT; i += 64) old[i] = ring[hp + i];
-    wave_sync();
-    for (uint32_t k = lane; k < 227; k += 64) nw[k] = old[k + 397] ^ mt_mix(old[k], old[k + 1]);
-    wave_sync();
-    for (uint32_t k = 227 + lane; k < 454; k += 64) nw[k] = nw[k - 227] ^ mt_mix(old[k], old[k + 1]);
-    wave_sync();
-    for (uint32_t k = 454 + lane; k < kMT; k += 64)
-        nw[k] = nw[k - 227] ^ mt_mix(old[k], k < kMT - 1 ? old[k + 1] : nw[0]);
-    wave_sync();
-    for (uint32_t i = lane; i < kMT; i += 64) ring[h + i] = nw[i];
-    wave_sync();
+    const uint32_t* old = ring + (kMT - h);
+    uint32_t* nw = ring + h;
+    uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t m = lane + 64 * j;
+        if (m < 227) a[j] = old[m + 397] ^ mt_mix(old[m], old[m + 1]);
+    }
+    const uint32_t n0 = __shfl(a[0], 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t m = lane + 64 * j;
+        if (m < 227) b[j] = a[j] ^ mt_mix(old[227 + m], old[228 + m]);
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const uint32_t m = lane + 64 * j;
+        if (m < 170) nw[454 + m] = b[j] ^ mt_mix(old[454 + m], m + 455 < kMT ? old[455 + m] : n0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t m = lane + 64 * j;
+        if (m < 227) nw[m] = a[j], nw[227 + m] = b[j];
+    }
 }
 
+// In-kernel refill for the RNG self-test: every lane with `need` gets its next block.
 // Must be called by every lane of the wave (wave-uniform control flow).
-__device__ void wave_refill(bool need, uint32_t slot, uint32_t& g, uint32_t* rings, uint32_t* lds, int lane) {
+__device__ void wave_refill(bool need, uint32_t slot, uint32_t& g, uint32_t* rings, int lane) {
     uint64_t m = __ballot(need);
     if (m == 0) return;
     while (m) {
@@ -107,10 +120,62 @@ __device__ void wave_refill(bool need, uint32_t slot, uint32_t& g, uint32_t* rin
         m &= m - 1;
         const uint32_t sl = __shfl(slot, L);
         const uint32_t gl = __shfl(g, L);
-        wave_twist(rings + (size_t)sl * kRing, gl, lds, lane);
+        wave_twist(rings + (size_t)sl * kRing, gl, lane);
     }
     if (need) g += kMT;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
+
+// Append v to list (count at cnt) for every lane with want set: one atomic per wave.
+// Must be called by every lane of the wave (wave-uniform control flow).
+__device__ __forceinline__ void wave_append(bool want, uint32_t v, uint32_t* list, uint32_t* cnt, int lane) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (want) list[base + __popcll(m & ((1ull << lane) - 1ull))] = v;
+}
+
+// Live and refill lists are partitioned: partition p owns the slots
+// [p*part_cap, (p+1)*part_cap) and its entries list[p*part_cap + i], i < count[p]; block b
+// serves partition b % n_part (grids are n_part * chunks blocks).  Appends then contend
+// on n_part counters instead of one, and a partition's slots are always touched by the
+// same XCD (blocks are dealt to the 8 XCDs round-robin and n_part is a multiple of 8).
+struct PartIter {
+    uint32_t p, first, stride, n;
+};
+__device__ __forceinline__ PartIter part_iter(const KParams& P, const uint32_t* count, uint32_t per_block) {
+    PartIter it;
+    it.p = blockIdx.x % P.n_part;
+    const uint32_t chunk = blockIdx.x / P.n_part, nchunks = gridDim.x / P.n_part;
+    it.first = chunk * per_block;
+    it.stride = nchunks * per_block;
+    it.n = count[it.p];
+    return it;
+}
+__device__ __forceinline__ void zero_parts(const KParams& P, uint32_t* c) {
+    if (blockIdx.x == 0 && threadIdx.x < P.n_part) c[threadIdx.x] = 0;
+}
+
+// k_refill: one wave per requested slot twists the next 624 words of its stream into the
+// consumed half of its ring (wave_twist), all requests in parallel across the chip.
+// Also clears the request counter the next epoch appends to.
+__global__ __launch_bounds__(kBlock) void k_refill(KParams P, const uint32_t* __restrict__ req,
+                                                    const uint32_t* __restrict__ count, uint32_t* zero_count) {
+    zero_parts(P, zero_count);
+    const PartIter it = part_iter(P, count, kBlock / 64);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint32_t i = it.first + wv; i < it.n; i += it.stride) {
+        const uint32_t s = req[it.p * P.part_cap + i];
+        const uint32_t g = P.rng_g[s];
+        wave_twist(P.ring + (size_t)s * kRing, g, lane);
+        if (lane == 0) {
+            P.rng_g[s] = g + kMT;
+            P.state[s] &= ~ST_RNGREQ;
+        }
+    }
 }
 
 // ====================================================================== geometry ====
@@ -174,7 +239,8 @@ __device__ __forceinline__ bool box_hit(v3 o, v3 d, v3 pmin, v3 pmax, float& t0,
 // mt19937::seed(j + width*i) for every slot (Src/renderer.cpp:35-36).  The recurrence is
 // serial per pixel, so each lane runs one pixel's recurrence and the wave writes the words
 // out through an LDS transpose (64 pixels x 64 words, padded row) as coalesced 256-B rows.
-__global__ __launch_bounds__(kBlock) void k_seed(KParams P, uint32_t* list, uint32_t* count, uint32_t* count_other) {
+__global__ __launch_bounds__(kBlock) void k_seed(KParams P, uint32_t* list, uint32_t* count, uint32_t* count_other,
+                                                  uint32_t* req_count) {
     __shared__ uint32_t lds[4][64][65];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t base = (blockIdx.x * kBlock) + wv * 64;
@@ -202,7 +268,8 @@ __global__ __launch_bounds__(kBlock) void k_seed(KParams P, uint32_t* list, uint
     if (valid) {
         P.rng_c[s] = kMT;   // cursor: next output is x[624]
         P.rng_g[s] = kMT;   // generated: x[0..623]
-        P.state[s] = ST_REGEN;
+        P.state[s] = ST_REGEN | ST_RNGREQ;   // first twist by the k_refill right after
+        P.req[s] = s;   // partition p = s / part_cap starts at p * part_cap: identity
         P.sample_k[s] = 0;
         P.depth[s] = 0;
         P.occ[s] = 0;
@@ -212,9 +279,13 @@ __global__ __launch_bounds__(kBlock) void k_seed(KParams P, uint32_t* list, uint
         P.c_stall[s] = 0;
         list[s] = s;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        *count = P.n_slots;
-        *count_other = 0;
+    if (blockIdx.x == 0 && threadIdx.x < P.n_part) {
+        const uint32_t p = threadIdx.x, lo = p * P.part_cap;
+        const uint32_t c = lo < P.n_slots ? min(P.part_cap, P.n_slots - lo) : 0u;
+        count[p] = c;
+        count_other[p] = 0;
+        req_count[p] = c;
+        req_count[kMaxParts + p] = 0;
     }
 }
 
@@ -225,13 +296,13 @@ __global__ __launch_bounds__(kBlock) void k_trace(KParams P, const uint32_t* __r
     __shared__ f4 lds_tri[SCN == SCN_SPHERE ? 1 : 3 * kTriTile];
     __shared__ f4 lds_sph[SCN == SCN_TRI ? 1 : kSphTile];
     __shared__ int lds_sobj[SCN == SCN_TRI ? 1 : kSphTile];
-    if (blockIdx.x == 0 && threadIdx.x == 0) *zero_count = 0;
-    const uint32_t n = *count;
+    zero_parts(P, zero_count);
+    const PartIter it = part_iter(P, count, kBlock);
     const int tid = threadIdx.x;
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    for (uint32_t base = it.first; base < it.n; base += it.stride) {
         const uint32_t i = base + tid;
-        const bool valid = i < n;
-        const uint32_t s = valid ? list[i] : 0;
+        const bool valid = i < it.n;
+        const uint32_t s = valid ? list[it.p * P.part_cap + i] : 0;
         const uint32_t st = valid ? P.state[s] : 0;
         const bool want = (st & ST_RAY) != 0;
         const uint32_t smask = (st >> ST_SHADOW_SHIFT) & ((1u << NL) - 1u);
@@ -371,16 +442,16 @@ __global__ __launch_bounds__(kBlock) void k_trace_small(KParams P, const uint32_
     extern __shared__ __attribute__((aligned(16))) f4 lds_small[];
     f4* ltri = lds_small;
     DObjBox* lbox = reinterpret_cast<DObjBox*>(lds_small + 3 * P.n_tris);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *zero_count = 0;
+    zero_parts(P, zero_count);
     const int tid = threadIdx.x;
     for (int q = tid; q < 3 * P.n_tris; q += kBlock) ltri[q] = P.tri[q];
     for (int q = tid; q < P.n_objs; q += kBlock) lbox[q] = P.obj_box[q];
     __syncthreads();
-    const uint32_t n = *count;
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    const PartIter it = part_iter(P, count, kBlock);
+    for (uint32_t base = it.first; base < it.n; base += it.stride) {
         const uint32_t i = base + tid;
-        const bool valid = i < n;
-        const uint32_t s = valid ? list[i] : 0;
+        const bool valid = i < it.n;
+        const uint32_t s = valid ? list[it.p * P.part_cap + i] : 0;
         const uint32_t st = valid ? P.state[s] : 0;
         const bool want = (st & ST_RAY) != 0;
         const uint32_t smask = (st >> ST_SHADOW_SHIFT) & ((1u << NL) - 1u);
@@ -697,21 +768,24 @@ __device__ int delta_track(const KParams& P, v3 o, v3 d, v3 thr, float& t, float
 template <int SCN, int INTEG>
 __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __restrict__ list,
                                                    const uint32_t* __restrict__ count, uint32_t* __restrict__ out,
-                                                   uint32_t* out_count) {
-    __shared__ uint32_t lds_twist[kBlock / 64][2 * kMT];
-    const uint32_t n = *count;
+                                                   uint32_t* out_count, uint32_t* req_count) {
+    const PartIter it = part_iter(P, count, kBlock);
     const int tid = threadIdx.x, lane = tid & 63;
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    for (uint32_t base = it.first; base < it.n; base += it.stride) {
         const uint32_t i = base + tid;
-        const bool valid = i < n;
-        const uint32_t s = valid ? list[i] : 0;
-        uint32_t g = valid ? P.rng_g[s] : 0;
+        const bool valid = i < it.n;
+        const uint32_t s = valid ? list[it.p * P.part_cap + i] : 0;
+        const uint32_t g = valid ? P.rng_g[s] : 0;
         Rng rng{P.ring + (size_t)s * kRing, valid ? P.rng_c[s] : 0};
-        wave_refill(valid && (g - rng.c) < kRngMin, s, g, P.ring, lds_twist[tid >> 6], lane);
-        if (valid) rng.prefetch(g - rng.c);
-
         uint32_t st = valid ? P.state[s] : ST_DONE;
-        if (valid) {
+        // RNG words: request a refill below kRngMin, sit this launch out below kRngVisit
+        const uint32_t avail = g - rng.c;
+        const bool want_req = valid && avail < kRngMin && !(st & ST_RNGREQ);
+        if (want_req) st |= ST_RNGREQ;
+        const bool go = valid && avail >= kRngVisit;
+        if (valid && !go && want_req) P.state[s] = st;
+        if (go) {
+            rng.prefetch(avail);
             uint32_t depth = P.depth[s];
             uint32_t k = P.sample_k[s];
             v3 thr = xyz(P.thr[s]), rad = xyz(P.rad[s]);
@@ -985,41 +1059,58 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
             P.thr[s] = pk(thr);
             P.rad[s] = pk(rad);
             P.rng_c[s] = rng.c;
-            P.rng_g[s] = g;
             if (nseg) P.c_seg[s] += nseg;
             if (nsh) P.c_shadow[s] += nsh;
             if (nrej) P.c_rej[s] += nrej;
             if (nstall) P.c_stall[s] += nstall;
         }
-        // ---- 4. compaction: ballot + prefix count, one atomic per wave
-        const bool keep = valid && !(st & ST_DONE);
-        const uint64_t m = __ballot(keep);
-        if (m) {
-            const uint32_t cnt = __popcll(m);
-            const uint32_t pre = __popcll(m & ((1ull << lane) - 1ull));
-            uint32_t wbase = 0;
-            if (lane == __ffsll((unsigned long long)m) - 1) wbase = atomicAdd(out_count, cnt);
-            wbase = __shfl(wbase, __ffsll((unsigned long long)m) - 1);
-            if (keep) out[wbase + pre] = s;
-        }
+        // ---- 4. compaction + refill requests: ballot + prefix count, one atomic per wave
+        wave_append(valid && !(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
+        wave_append(want_req, s, P.req + it.p * P.part_cap, req_count + it.p, lane);
     }
 }
 
+// LDS carve of the fused schedule (bytes; every f4 region 16-aligned): triangles, their
+// geometric and vertex normals, per-object culling boxes (triangle scenes), spheres,
+// medium boxes, the object and light tables, sphere->object map.
+struct StepLayout {
+    uint32_t tri, tng, nrm, box, sph, bx, obj, light, sobj, total;
+};
+__host__ __device__ inline StepLayout step_layout(const KParams& P) {
+    StepLayout L;
+    L.tri = 0;
+    L.tng = L.tri + 48u * P.n_tris;
+    L.nrm = L.tng + 16u * P.n_tris;
+    L.box = L.nrm + 48u * P.n_tris;
+    L.sph = L.box + (P.scene_kind == SCN_TRI ? 32u * P.n_objs : 0u);
+    L.bx = L.sph + 16u * P.n_sph;
+    L.obj = L.bx + 32u * P.n_box;
+    L.light = L.obj + (uint32_t)sizeof(DObj) * P.n_objs;
+    L.sobj = L.light + (uint32_t)sizeof(DLight) * P.n_lights;
+    L.total = L.sobj + 4u * P.n_sph;
+    return L;
+}
+
 // ============================================================ fused schedule ====
-// k_step: one launch per iteration over the compacted live list; per slot it traces the
-// pending ray, shades the hit (NEE shadow rays are traced immediately, so no shadow state
-// crosses a launch), and finalises/regenerates — the per-pixel sequence of
-// NormalRenderer::doRender + integrate(), one bounce per launch.  The whole scene
-// (triangle geometry and normals' plane, spheres, boxes) lives in LDS, so it is used for
-// scenes up to kStepTris triangles / kStepSph spheres (C1, C2, C3, C5); larger scenes use
-// the multi-pass wavefront (k_shade / k_trace with LDS tiles).
+// k_step: per live slot, up to `visits` path segments in one launch with the path state in
+// registers: trace the pending ray, shade the hit (NEE shadow rays traced immediately, so
+// no shadow state crosses a segment), finish/regenerate samples — the per-pixel sequence
+// of NormalRenderer::doRender + integrate().  The scene and its tables live in LDS
+// (step_layout), so this schedule serves scenes up to kStepLds bytes (C1, C2, C3, C5);
+// larger scenes use the multi-pass wavefront (k_shade / k_trace with LDS tiles).  A slot
+// stops early when its RNG ring runs low or it is done; at the end of the launch the slot
+// is appended to the next round's live list and, when fewer than kRngKeep words are left,
+// to the refill list k_refill services between rounds.
 struct LScene {
     const f4* tri;      // 3 per triangle
     const f4* tng;      // geometric normal per triangle
+    const f4* nrm;      // 3 vertex normals per triangle
     const DObjBox* box; // per object (SCN_TRI)
     const f4* sph;
     const int* sobj;
     const f4* bx;       // 2 per box
+    const DObj* obj;
+    const DLight* light;
 };
 
 struct HitRec {
@@ -1125,9 +1216,14 @@ __device__ __forceinline__ bool occluded_l(const KParams& P, const LScene& L, v3
     }
 }
 
+__device__ __forceinline__ v3 tri_ns_l(const LScene& L, int i, float u, float v) {
+    const float w = 1.0f - u - v;
+    return xyz(L.nrm[3 * i]) * w + xyz(L.nrm[3 * i + 1]) * u + xyz(L.nrm[3 * i + 2]) * v;
+}
+
 // IntersectInfo::surfaceInfo from a hit record (see surface<>)
 template <int SCN>
-__device__ __forceinline__ int surface_l(const KParams& P, const LScene& L, v3 o, v3 d, const HitRec& h, Surf& S) {
+__device__ __forceinline__ int surface_l(const LScene& L, v3 o, v3 d, const HitRec& h, Surf& S) {
     S.pos = S.ng = S.ns = S.dpdu = S.dpdv = mk(0, 0, 0);
     if (h.code < 0) return -1;
     int surf = h.code, dp = (SCN == SCN_TRI) ? h.code : -1;
@@ -1138,88 +1234,92 @@ __device__ __forceinline__ int surface_l(const KParams& P, const LScene& L, v3 o
         S.pos = ray_at(o, d, st);
         if (kind == SEG_TRI) {
             S.ng = xyz(L.tng[idx]);
-            S.ns = tri_ns(P, idx, su, sv);
+            S.ns = tri_ns_l(L, idx, su, sv);
         } else {
             S.ng = normalize(ray_at(o, d, st) - xyz(L.sph[idx]));
             S.ns = S.ng;
         }
     }
-    if (dp >= 0) onb(tri_ns(P, dp & 0x0fffffff, du, dv), S.dpdu, S.dpdv);
+    if (dp >= 0) onb(tri_ns_l(L, dp & 0x0fffffff, du, dv), S.dpdu, S.dpdv);
     const int kind = h.code >> 28, idx = h.code & 0x0fffffff;
     if (kind == SEG_TRI) return __float_as_int(L.tri[3 * idx].w);
     if (kind == SEG_SPHERE) return L.sobj[idx] & 0x3fffffff;
     return __float_as_int(L.bx[2 * idx].w);
 }
 
+template <typename T>
+__device__ __forceinline__ void lds_copy(T* dst, const T* src, int n, int tid) {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+    const int words = n * (int)(sizeof(T) / 4);
+    for (int q = tid; q < words; q += kBlock) d[q] = s[q];
+}
+
 template <int SCN, int INTEG>
 __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __restrict__ list,
                                                   const uint32_t* __restrict__ count, uint32_t* __restrict__ out,
-                                                  uint32_t* out_count, uint32_t* zero_count) {
+                                                  uint32_t* out_count, uint32_t* zero_count, uint32_t* req_count,
+                                                  uint32_t visits) {
     extern __shared__ __attribute__((aligned(16))) f4 lds_step[];
-    // carve: twist scratch | tri | tng | boxes | spheres | sphere objects | medium boxes
-    uint32_t* lds_twist = reinterpret_cast<uint32_t*>(lds_step);
-    f4* p = lds_step + (kBlock / 64) * 2 * kMT / 4;
+    char* lb = reinterpret_cast<char*>(lds_step);
+    const StepLayout Lo = step_layout(P);
     LScene L;
-    L.tri = p;
-    p += 3 * P.n_tris;
-    L.tng = p;
-    p += P.n_tris;
-    L.box = reinterpret_cast<const DObjBox*>(p);
-    p += (SCN == SCN_TRI ? 2 * P.n_objs : 0);
-    L.sph = p;
-    p += P.n_sph;
-    L.bx = p;
-    p += 2 * P.n_box;
-    L.sobj = reinterpret_cast<const int*>(p);
-    const int tid = threadIdx.x, lane = tid & 63;
-    {
-        f4* w = const_cast<f4*>(L.tri);
-        for (int q = tid; q < 3 * P.n_tris; q += kBlock) w[q] = P.tri[q];
-        w = const_cast<f4*>(L.tng);
-        for (int q = tid; q < P.n_tris; q += kBlock) w[q] = P.tri_ng[q];
-        if (SCN == SCN_TRI) {
-            DObjBox* wb = const_cast<DObjBox*>(L.box);
-            for (int q = tid; q < P.n_objs; q += kBlock) wb[q] = P.obj_box[q];
-        }
-        w = const_cast<f4*>(L.sph);
-        for (int q = tid; q < P.n_sph; q += kBlock) w[q] = P.sph[q];
-        int* wo = const_cast<int*>(L.sobj);
-        for (int q = tid; q < P.n_sph; q += kBlock) wo[q] = P.sph_obj[q];
-        w = const_cast<f4*>(L.bx);
-        for (int q = tid; q < 2 * P.n_box; q += kBlock) w[q] = P.box[q];
-    }
-    if (blockIdx.x == 0 && tid == 0) *zero_count = 0;
+    L.tri = reinterpret_cast<const f4*>(lb + Lo.tri);
+    L.tng = reinterpret_cast<const f4*>(lb + Lo.tng);
+    L.nrm = reinterpret_cast<const f4*>(lb + Lo.nrm);
+    L.box = reinterpret_cast<const DObjBox*>(lb + Lo.box);
+    L.sph = reinterpret_cast<const f4*>(lb + Lo.sph);
+    L.bx = reinterpret_cast<const f4*>(lb + Lo.bx);
+    L.obj = reinterpret_cast<const DObj*>(lb + Lo.obj);
+    L.light = reinterpret_cast<const DLight*>(lb + Lo.light);
+    L.sobj = reinterpret_cast<const int*>(lb + Lo.sobj);
+    const int tid = threadIdx.x;
+    lds_copy(const_cast<f4*>(L.tri), P.tri, 3 * P.n_tris, tid);
+    lds_copy(const_cast<f4*>(L.tng), P.tri_ng, P.n_tris, tid);
+    lds_copy(const_cast<f4*>(L.nrm), P.tri_nrm, 3 * P.n_tris, tid);
+    if (SCN == SCN_TRI) lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid);
+    lds_copy(const_cast<f4*>(L.sph), P.sph, P.n_sph, tid);
+    lds_copy(const_cast<f4*>(L.bx), P.box, 2 * P.n_box, tid);
+    lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
+    lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid);
+    lds_copy(const_cast<int*>(L.sobj), P.sph_obj, P.n_sph, tid);
     __syncthreads();
-    const uint32_t n = *count;
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    zero_parts(P, zero_count);
+    const int lane = tid & 63;
+    const PartIter it = part_iter(P, count, kBlock);
+    for (uint32_t base = it.first; base < it.n; base += it.stride) {
         const uint32_t i = base + tid;
-        const bool valid = i < n;
-        const uint32_t s = valid ? list[i] : 0;
-        uint32_t g = valid ? P.rng_g[s] : 0;
-        Rng rng{P.ring + (size_t)s * kRing, valid ? P.rng_c[s] : 0};
-        wave_refill(valid && (g - rng.c) < kRngMin, s, g, P.ring, lds_twist + (tid >> 6) * 2 * kMT, lane);
-        uint32_t st = valid ? P.state[s] : ST_DONE;
-        if (valid) {
+        const uint32_t s = i < it.n ? list[it.p * P.part_cap + i] : 0;
+        uint32_t st = i < it.n ? P.state[s] : ST_DONE;
+        bool want_req = false;
+        if (!(st & ST_DONE)) {
+        const uint32_t g = P.rng_g[s];
+        Rng rng{P.ring + (size_t)s * kRing, P.rng_c[s]};
+        uint32_t depth = P.depth[s];
+        uint32_t k = P.sample_k[s];
+        v3 thr = mk(1, 1, 1), rad = mk(0, 0, 0), o = mk(0, 0, 0), d = mk(0, 0, 0);
+        if (!(st & ST_REGEN)) {
+            thr = xyz(P.thr[s]), rad = xyz(P.rad[s]);
+            o = xyz(P.ray_o[s]), d = xyz(P.ray_d[s]);
+        }
+        uint32_t nseg = 0, nsh = 0, nrej = 0, nstall = 0;
+        const uint32_t col = s % P.width, row = P.shard_index + P.shard_count * (s / P.width);
+        float* px = P.fb + 3 * ((size_t)col + (size_t)P.width * row);
+        for (uint32_t vis = 0; vis < visits; ++vis) {
+            if ((st & ST_DONE) || g - rng.c < kRngVisit) break;
             rng.prefetch(g - rng.c);
-            uint32_t depth = P.depth[s];
-            uint32_t k = P.sample_k[s];
-            v3 thr = mk(1, 1, 1), rad = mk(0, 0, 0), o, d;
-            uint32_t nseg = 0, nsh = 0, nrej = 0, nstall = 0;
-            const uint32_t col = s % P.width, row = P.shard_index + P.shard_count * (s / P.width);
-            bool ended = false, trace = false;
+            bool ended = false, trace = true;
             if (st & ST_REGEN) {
                 // next sample: jitter draws + camera ray (Src/renderer.cpp:44-50)
                 st &= ~ST_REGEN;
                 const float u = ((float)(int)col + rng.next()) / (float)P.width;
                 const float v = ((float)(int)row + rng.next()) / (float)P.height;
                 camera_ray(P, u, v, o, d);
+                thr = mk(1, 1, 1), rad = mk(0, 0, 0);
                 depth = 0;
-                if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) ended = true;
-                else trace = true;
-            } else {
-                thr = xyz(P.thr[s]), rad = xyz(P.rad[s]);
-                o = xyz(P.ray_o[s]), d = xyz(P.ray_d[s]);
-                trace = !(st & ST_MEDIUM);
+                if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) ended = true, trace = false;
+            } else if (INTEG == XRT_INTEGRATOR_VPT && (st & ST_MEDIUM)) {
+                trace = false;
             }
             bool walk = false;
             float mt = 0.0f, mt1 = 0.0f;
@@ -1235,19 +1335,19 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
                 HitRec h;
                 closest_l<SCN>(P, L, o, d, h);
                 Surf S;
-                const int obj = surface_l<SCN>(P, L, o, d, h, S);
+                const int obj = surface_l<SCN>(L, o, d, h, S);
                 if (INTEG == XRT_INTEGRATOR_DIRECT) {
                     // DirectIntegrator::integrate (Src/integrator.h:82-119)
                     if (obj < 0) {
                         rad = mk((float)0.18, (float)0.18, (float)0.18);
-                    } else if (P.objs[obj].light >= 0) {
-                        rad = light_Le(P.lights[P.objs[obj].light], S.ns, d);
+                    } else if (L.obj[obj].light >= 0) {
+                        rad = light_Le(L.light[L.obj[obj].light], S.ns, d);
                     } else {
-                        const DObj ob = P.objs[obj];
+                        const DObj& ob = L.obj[obj];
                         for (int l = 0; l < P.n_lights; ++l) {
                             v3 wi = mk(0, 0, 0);
                             float tmax = 0.0f, pdf = 0.0f;
-                            const v3 Lv = light_sample(P.lights[l], S.pos, wi, pdf, tmax, rng);
+                            const v3 Lv = light_sample(L.light[l], S.pos, wi, pdf, tmax, rng);
                             if (pdf == 0.0f) continue;
                             const float bias = 0.01f;
                             ++nsh;
@@ -1270,9 +1370,9 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
                             if (rng.next() >= pr) alive = false, ended = true;
                             else thr = thr / mk(pr, pr, pr);
                         }
-                        const DObj ob = P.objs[obj];
+                        const DObj& ob = L.obj[obj];
                         if (alive && ob.light >= 0) {
-                            rad = rad + thr * light_Le(P.lights[ob.light], S.ns, d);
+                            rad = rad + thr * light_Le(L.light[ob.light], S.ns, d);
                             alive = false, ended = true;
                         }
                         if (alive) {
@@ -1281,7 +1381,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
                                 sa = ld3(P.medium.absorption) * medium_density(P.medium, ray_at(o, d, mt));
                                 walk = true;
                             } else {
-                                ++nstall;
+                                ++nstall;   // see k_shade: the reference never advances this ray
                                 ended = true;
                             }
                         }
@@ -1298,9 +1398,9 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
                             if (rng.next() >= pr) alive = false, ended = true;
                             else thr = thr / mk(pr, pr, pr);
                         }
-                        const DObj ob = P.objs[obj];
+                        const DObj& ob = L.obj[obj];
                         if (alive && ob.light >= 0) {
-                            if (depth == 0) rad = rad + thr * light_Le(P.lights[ob.light], S.ns, d);
+                            if (depth == 0) rad = rad + thr * light_Le(L.light[ob.light], S.ns, d);
                             alive = false, ended = true;
                         }
                         if (alive) {
@@ -1309,7 +1409,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
                                 v3 L_light = mk(0, 0, 0);
                                 v3 wi = mk(0, 0, 0);
                                 float tmax = 0.0f, pdf = 0.0f;
-                                const v3 Lv = light_sample(P.lights[l], S.pos, wi, pdf, tmax, rng);
+                                const v3 Lv = light_sample(L.light[l], S.pos, wi, pdf, tmax, rng);
                                 if (pdf == 0.0f) continue;
                                 const float bias = 0.01f;
                                 ++nsh;
@@ -1351,7 +1451,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
                     if (depth >= P.max_depth) ended = true;
                 }
             }
-            // finish the sample (Src/renderer.cpp:55-75); the next one starts next launch
+            // finish the sample (Src/renderer.cpp:55-75); the next one starts next segment
             while (ended) {
                 ended = false;
                 const v3 r = rad / 1.0f;
@@ -1359,7 +1459,6 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
                     __builtin_isinf(r.y) || __builtin_isinf(r.z) || r.x < 0.0f || r.y < 0.0f || r.z < 0.0f) {
                     ++nrej;
                 } else {
-                    float* px = P.fb + 3 * ((size_t)col + (size_t)P.width * row);
                     px[0] = px[0] + r.x, px[1] = px[1] + r.y, px[2] = px[2] + r.z;
                 }
                 ++k;
@@ -1373,33 +1472,28 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
                     st |= ST_REGEN;
                 }
             }
-            P.state[s] = st;
-            if (!(st & (ST_DONE | ST_REGEN))) {
-                P.depth[s] = depth;
-                P.thr[s] = pk(thr);
-                P.rad[s] = pk(rad);
-                P.ray_o[s] = pk(o);
-                P.ray_d[s] = pk(d);
-            }
-            P.sample_k[s] = k;
-            P.rng_c[s] = rng.c;
-            P.rng_g[s] = g;
-            if (nseg) P.c_seg[s] += nseg;
-            if (nsh) P.c_shadow[s] += nsh;
-            if (nrej) P.c_rej[s] += nrej;
-            if (nstall) P.c_stall[s] += nstall;
         }
-        const bool keep = valid && !(st & ST_DONE);
-        const uint64_t m = __ballot(keep);
-        if (m) {
-            const uint32_t cnt = __popcll(m);
-            const uint32_t pre = __popcll(m & ((1ull << lane) - 1ull));
-            const int leader = __ffsll((unsigned long long)m) - 1;
-            uint32_t wbase = 0;
-            if (lane == leader) wbase = atomicAdd(out_count, cnt);
-            wbase = __shfl(wbase, leader);
-            if (keep) out[wbase + pre] = s;
+        // queue an RNG refill for k_refill (Rng words ahead < kRngKeep, once per request)
+        want_req = !(st & (ST_DONE | ST_RNGREQ)) && g - rng.c < kRngKeep;
+        if (want_req) st |= ST_RNGREQ;
+        P.state[s] = st;
+        if (!(st & (ST_DONE | ST_REGEN))) {
+            P.depth[s] = depth;
+            P.thr[s] = pk(thr);
+            P.rad[s] = pk(rad);
+            P.ray_o[s] = pk(o);
+            P.ray_d[s] = pk(d);
         }
+        P.sample_k[s] = k;
+        P.rng_c[s] = rng.c;
+        if (nseg) P.c_seg[s] += nseg;
+        if (nsh) P.c_shadow[s] += nsh;
+        if (nrej) P.c_rej[s] += nrej;
+        if (nstall) P.c_stall[s] += nstall;
+        }
+        // live list of the next round and refill requests (partitioned, one atomic per wave)
+        wave_append(!(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
+        wave_append(want_req, s, P.req + it.p * P.part_cap, req_count + it.p, lane);
     }
 }
 
@@ -1437,7 +1531,6 @@ __global__ __launch_bounds__(kBlock) void k_finish(KParams P) {
 // ============================================================== self-tests ====
 __global__ __launch_bounds__(kBlock) void k_test_rng(const uint32_t* seeds, uint32_t n_seeds, uint32_t skip,
                                                       uint32_t n, float* out, uint32_t* rings) {
-    __shared__ uint32_t lds_twist[kBlock / 64][2 * kMT];
     const int lane = threadIdx.x & 63;
     const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     const bool valid = s < n_seeds;
@@ -1456,7 +1549,7 @@ __global__ __launch_bounds__(kBlock) void k_test_rng(const uint32_t* seeds, uint
     // consume skip + n draws, refilling cooperatively like k_shade does
     const uint32_t total = skip + n;
     for (uint32_t done = 0; done < total;) {
-        wave_refill(valid && (g - rng.c) < kRngMin, s, g, rings, lds_twist[threadIdx.x >> 6], lane);
+        wave_refill(valid && (g - rng.c) < kRngMin, s, g, rings, lane);
         const uint32_t chunk = min(32u, total - done);   // < kRngMin: never reads past g
         if (valid) {
             for (uint32_t q = 0; q < chunk; ++q) {
@@ -1506,9 +1599,17 @@ __global__ void k_test_logexp(const float* x, uint32_t n, float* out) {
 
 namespace xrt {
 
-hipError_t launch_seed(const KParams& P, uint32_t* list, uint32_t* count, uint32_t* count_other, hipStream_t st) {
+hipError_t launch_seed(const KParams& P, uint32_t* list, uint32_t* count, uint32_t* count_other,
+                       uint32_t* req_count, hipStream_t st) {
     const uint32_t blocks = (P.n_slots + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k_seed, dim3(blocks), dim3(kBlock), 0, st, P, list, count, count_other);
+    hipLaunchKernelGGL(k_seed, dim3(blocks), dim3(kBlock), 0, st, P, list, count, count_other, req_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_refill(const KParams& P, const uint32_t* count, uint32_t* zero_count, hipStream_t st) {
+    const uint32_t per = std::max<uint32_t>(1u, std::min<uint32_t>((P.part_cap + 3) / 4, 2048u / P.n_part));
+    const uint32_t blocks = P.n_part * per;
+    hipLaunchKernelGGL(k_refill, dim3(blocks), dim3(kBlock), 0, st, P, P.req, count, zero_count);
     return hipGetLastError();
 }
 
@@ -1542,61 +1643,60 @@ hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* 
 
 template <int SCN>
 static hipError_t shade_i(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
-                          uint32_t* out_count, uint32_t blocks, hipStream_t st) {
+                          uint32_t* out_count, uint32_t* req_count, uint32_t blocks, hipStream_t st) {
     if (P.integrator == XRT_INTEGRATOR_DIRECT)
         hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_DIRECT>), dim3(blocks), dim3(kBlock), 0, st, P, list,
-                           count, out, out_count);
+                           count, out, out_count, req_count);
     else if (P.integrator == XRT_INTEGRATOR_VPT)
         hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_VPT>), dim3(blocks), dim3(kBlock), 0, st, P, list, count,
-                           out, out_count);
+                           out, out_count, req_count);
     else
         hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_GI>), dim3(blocks), dim3(kBlock), 0, st, P, list, count,
-                           out, out_count);
+                           out, out_count, req_count);
     return hipGetLastError();
 }
 
 hipError_t launch_shade(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
-                        uint32_t* out_count, uint32_t blocks, hipStream_t st) {
+                        uint32_t* out_count, uint32_t* req_count, uint32_t blocks, hipStream_t st) {
     switch (P.scene_kind) {
-        case SCN_TRI: return shade_i<SCN_TRI>(P, list, count, out, out_count, blocks, st);
-        case SCN_SPHERE: return shade_i<SCN_SPHERE>(P, list, count, out, out_count, blocks, st);
-        default: return shade_i<SCN_MIXED>(P, list, count, out, out_count, blocks, st);
+        case SCN_TRI: return shade_i<SCN_TRI>(P, list, count, out, out_count, req_count, blocks, st);
+        case SCN_SPHERE: return shade_i<SCN_SPHERE>(P, list, count, out, out_count, req_count, blocks, st);
+        default: return shade_i<SCN_MIXED>(P, list, count, out, out_count, req_count, blocks, st);
     }
 }
 
 size_t step_lds_bytes(const KParams& P) {
     if (P.scene_kind == SCN_TRI && !P.small_tri) return 0;   // needs the per-object boxes
-    const size_t twist = (kBlock / 64) * 2 * kMT * sizeof(uint32_t);
-    const size_t scene = sizeof(f4) * (4 * (size_t)P.n_tris + (P.scene_kind == SCN_TRI ? 2 * (size_t)P.n_objs : 0) +
-                                       (size_t)P.n_sph + 2 * (size_t)P.n_box) +
-                         sizeof(int) * (size_t)P.n_sph;
-    const size_t total = twist + scene;
-    return total <= kStepLds ? total : 0;
+    if (P.n_tris > 65536 || P.n_sph > 65536 || P.n_box > 65536 || P.n_objs > 65536) return 0;
+    const size_t total = step_layout(P).total;
+    return total <= kStepLds ? (total + 15) / 16 * 16 : 0;
 }
 
 template <int SCN>
 static hipError_t step_i(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
-                         uint32_t* out_count, uint32_t* zero, uint32_t blocks, hipStream_t st) {
+                         uint32_t* out_count, uint32_t* zero, uint32_t* req_count, uint32_t visits, uint32_t blocks,
+                         hipStream_t st) {
     const size_t lds = step_lds_bytes(P);
     if (P.integrator == XRT_INTEGRATOR_DIRECT)
         hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_DIRECT>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
-                           out, out_count, zero);
+                           out, out_count, zero, req_count, visits);
     else if (P.integrator == XRT_INTEGRATOR_VPT)
         hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_VPT>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
-                           out, out_count, zero);
+                           out, out_count, zero, req_count, visits);
     else
         hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_GI>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
-                           out, out_count, zero);
+                           out, out_count, zero, req_count, visits);
     return hipGetLastError();
 }
 
 hipError_t launch_step(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
-                       uint32_t* out_count, uint32_t* zero, uint32_t blocks, hipStream_t st) {
+                       uint32_t* out_count, uint32_t* zero, uint32_t* req_count, uint32_t visits, uint32_t blocks,
+                       hipStream_t st) {
     if (!step_lds_bytes(P)) return hipErrorInvalidValue;
     switch (P.scene_kind) {
-        case SCN_TRI: return step_i<SCN_TRI>(P, list, count, out, out_count, zero, blocks, st);
-        case SCN_SPHERE: return step_i<SCN_SPHERE>(P, list, count, out, out_count, zero, blocks, st);
-        default: return step_i<SCN_MIXED>(P, list, count, out, out_count, zero, blocks, st);
+        case SCN_TRI: return step_i<SCN_TRI>(P, list, count, out, out_count, zero, req_count, visits, blocks, st);
+        case SCN_SPHERE: return step_i<SCN_SPHERE>(P, list, count, out, out_count, zero, req_count, visits, blocks, st);
+        default: return step_i<SCN_MIXED>(P, list, count, out, out_count, zero, req_count, visits, blocks, st);
     }
 }
 

@@ -111,7 +111,7 @@ int xrt_create(int device, xrt_ctx** out) {
     xrt_ctx* c = new xrt_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&c->h_poll, 64 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc((void**)&c->h_poll, 8 * kMaxParts * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
         delete c;
         return XRT_ERR_HIP;
     }
@@ -347,11 +347,11 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             (rc = ensure(c, c->occ, n * 4)) || (rc = ensure(c, c->rng_c, n * 4)) || (rc = ensure(c, c->rng_g, n * 4)) ||
             (rc = ensure(c, c->ring, n * kRing * 4)) || (rc = ensure(c, c->c_seg, n * 4)) ||
             (rc = ensure(c, c->c_shadow, n * 4)) || (rc = ensure(c, c->c_rej, n * 4)) || (rc = ensure(c, c->c_stall, n * 4)) ||
-            (rc = ensure(c, c->lists, 2 * n * 4)))
+            (rc = ensure(c, c->lists, 3 * (n + kMaxParts) * 4)))   // two live lists + the refill list
             return rc;
         c->cap_slots = n;
     }
-    if ((rc = ensure(c, c->counts, 64)) || (rc = ensure(c, c->stats, 64))) return rc;
+    if ((rc = ensure(c, c->counts, 5 * kMaxParts * 4)) || (rc = ensure(c, c->stats, 64))) return rc;
     float* fb = d_out;
     if (!fb) {
         if ((rc = ensure(c, c->fb, npix * 3 * sizeof(float)))) return rc;
@@ -361,6 +361,14 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     P.integrator = p->integrator;
     P.max_depth = p->max_depth, P.width = p->width, P.height = p->height, P.spp = p->spp;
     P.shard_index = p->shard_index, P.shard_count = p->shard_count, P.n_slots = (uint32_t)n;
+    // live-list partitions: up to kMaxParts (a multiple of the 8 XCDs), >= 2048 slots each
+    {
+        uint32_t np = (uint32_t)std::min<size_t>(kMaxParts, std::max<size_t>(1, n / 2048));
+        if (np >= 8) np &= ~7u;
+        P.n_part = np;
+        P.part_cap = (uint32_t)((n + np - 1) / np);
+    }
+    const size_t lcap = (size_t)P.n_part * P.part_cap;
     P.ray_o = as<f4>(c->ray_o), P.ray_d = as<f4>(c->ray_d), P.thr = as<f4>(c->thr), P.rad = as<f4>(c->rad);
     P.thr_prev = as<f4>(c->thr_prev), P.hit = as<f4>(c->hit), P.hit2 = as<f4>(c->hit2), P.hit3 = as<f4>(c->hit3);
     P.sh_o = as<f4>(c->sh_o), P.sh_d = as<f4>(c->sh_d), P.sh_c = as<f4>(c->sh_c);
@@ -373,8 +381,12 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     P.fb = fb;
     P.stats = as<unsigned long long>(c->stats);
 
-    uint32_t* lists[2] = {as<uint32_t>(c->lists), as<uint32_t>(c->lists) + n};
-    uint32_t* counts = as<uint32_t>(c->counts);
+    uint32_t* lists[2] = {as<uint32_t>(c->lists), as<uint32_t>(c->lists) + lcap};
+    P.req = as<uint32_t>(c->lists) + 2 * lcap;
+    // counter arrays of kMaxParts words: live[0..2] (rotating), then refill[0..1]
+    uint32_t* cbase = as<uint32_t>(c->counts);
+    auto counts_at = [&](uint64_t j) { return cbase + (size_t)j * kMaxParts; };
+    uint32_t* req_counts = cbase + 3 * kMaxParts;
     const bool timing = (p->flags & XRT_FLAG_TIMING) != 0;
     xrt_stats S;
     std::memset(&S, 0, sizeof(S));
@@ -404,9 +416,21 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
 
     HIPCHK(c, hipMemsetAsync(fb, 0, npix * 3 * sizeof(float), c->stream));
     HIPCHK(c, hipMemsetAsync(P.stats, 0, 64, c->stream));
-    HIPCHK(c, launch(XRT_K_SEED, [&] { return launch_seed(P, lists[0], counts + 0, counts + 1, c->stream); }));
+    HIPCHK(c, launch(XRT_K_SEED, [&] { return launch_seed(P, lists[0], counts_at(0), counts_at(1), req_counts, c->stream); }));
+    // refill epochs: shading launches of epoch e append to req_counts[e & 1]; k_refill(e)
+    // consumes it and clears req_counts[(e + 1) & 1] for epoch e + 1.  Epoch 0 is the
+    // first twist of every slot, requested by k_seed.
+    uint64_t epoch = 0;
+    auto refill = [&]() -> hipError_t {
+        const int a = (int)(epoch & 1), b = a ^ 1;
+        ++epoch;
+        return launch(XRT_K_REFILL, [&] {
+            return launch_refill(P, req_counts + a * kMaxParts, req_counts + b * kMaxParts, c->stream);
+        });
+    };
+    HIPCHK(c, refill());
 
-    const uint32_t blocks = (uint32_t)std::min<size_t>((n + 255) / 256, 8192);
+    const uint32_t blocks = P.n_part * ((P.part_cap + 255) / 256);   // one entry per thread
     // GI/Direct: at most max_depth + 1 shade passes per sample; VPT walks are unbounded
     // (null collisions, suspensions), so only the live-slot poll ends the loop there.
     const uint64_t cap_iters = p->integrator == XRT_INTEGRATOR_VPT ? (uint64_t)p->spp * 100000ull + 1000000ull
@@ -425,47 +449,61 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     uint64_t it = 0;
     int poll_slot = 0;
     bool done = false;
-    // Schedule: the fused k_step (scene resident in LDS, one launch per bounce) when the
-    // scene fits, else the multi-pass wavefront (k_shade, then k_trace streaming the scene
-    // through LDS tiles).  k_step rotates three live counters: launch i reads counts[i%3],
-    // appends to counts[(i+1)%3] and clears counts[(i+2)%3] for launch i+1.
+    // Schedule: the fused k_step (scene resident in LDS, kStepVisits path segments per
+    // slot per launch, in-kernel compaction and refill requests; k_refill every
+    // kStepRefill rounds) when the scene fits, else the multi-pass wavefront (k_shade, then
+    // k_trace streaming the scene through LDS tiles, k_refill every kRefillEvery
+    // iterations).  k_step rotates three live counters: round i reads counts[i%3], appends
+    // to counts[(i+1)%3] and clears counts[(i+2)%3] for round i+1.
     const bool fused = !(p->flags & XRT_FLAG_WAVEFRONT) && step_lds_bytes(P) != 0;
+    const uint64_t poll_every = fused ? 4 : kPoll, ahead = fused ? 16 : kAhead;
     for (; it < cap_iters && !done; ++it) {
         const int cur = (int)(it & 1), nxt = cur ^ 1;
         uint32_t* live = nullptr;
         if (fused) {
             const int ci = (int)(it % 3), co = (int)((it + 1) % 3), cz = (int)((it + 2) % 3);
-            live = counts + co;
+            live = counts_at(co);
             hipError_t e = launch(XRT_K_STEP, [&] {
-                return launch_step(P, lists[cur], counts + ci, lists[nxt], counts + co, counts + cz, blocks, c->stream);
+                return launch_step(P, lists[cur], counts_at(ci), lists[nxt], counts_at(co), counts_at(cz),
+                                   req_counts + (epoch & 1) * kMaxParts, kStepVisits, blocks, c->stream);
             });
             if (e != hipSuccess) return hip_err(c, e, "k_step");
+            if (it % kStepRefill == kStepRefill - 1) {
+                e = refill();
+                if (e != hipSuccess) return hip_err(c, e, "k_refill");
+            }
         } else {
-            live = counts + nxt;
+            live = counts_at(nxt);
             hipError_t e = launch(XRT_K_SHADE, [&] {
-                return launch_shade(P, lists[cur], counts + cur, lists[nxt], counts + nxt, blocks, c->stream);
+                return launch_shade(P, lists[cur], counts_at(cur), lists[nxt], counts_at(nxt),
+                                    req_counts + (epoch & 1) * kMaxParts, blocks, c->stream);
             });
             if (e != hipSuccess) return hip_err(c, e, "k_shade");
-        }
-        if (it % kPoll == kPoll - 1) {
-            const int ps = poll_slot++ % 8;
-            HIPCHK(c, hipMemcpyAsync(c->h_poll + ps, live, 4, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(c, hipEventRecord(poll_ev[ps], c->stream));
-            polls.push_back({it, poll_ev[ps], ps});
-        }
-        if (!fused) {
-            hipError_t e = launch(XRT_K_TRACE, [&] {
-                return launch_trace(P, lists[nxt], counts + nxt, counts + cur, blocks, c->stream);
+            e = launch(XRT_K_TRACE, [&] {
+                return launch_trace(P, lists[nxt], counts_at(nxt), counts_at(cur), blocks, c->stream);
             });
             if (e != hipSuccess) return hip_err(c, e, "k_trace");
+            if (it % kRefillEvery == kRefillEvery - 1) {
+                e = refill();
+                if (e != hipSuccess) return hip_err(c, e, "k_refill");
+            }
+        }
+        if (it % poll_every == poll_every - 1) {
+            const int ps = poll_slot++ % 8;
+            HIPCHK(c, hipMemcpyAsync(c->h_poll + ps * kMaxParts, live, P.n_part * 4, hipMemcpyDeviceToHost,
+                                     c->stream));
+            HIPCHK(c, hipEventRecord(poll_ev[ps], c->stream));
+            polls.push_back({it, poll_ev[ps], ps});
         }
         // retire polls: non-blocking when possible, blocking when too far ahead
         while (!polls.empty()) {
             Poll& q = polls.front();
-            const bool must_wait = it - q.it >= kAhead;
+            const bool must_wait = it - q.it >= ahead;
             if (!must_wait && hipEventQuery(q.ev) != hipSuccess) break;
             HIPCHK(c, hipEventSynchronize(q.ev));
-            if (c->h_poll[q.slot] == 0) done = true;
+            uint64_t alive = 0;
+            for (uint32_t k = 0; k < P.n_part; ++k) alive += c->h_poll[q.slot * kMaxParts + k];
+            if (alive == 0) done = true;
             polls.erase(polls.begin());
             if (done) break;
         }
@@ -476,9 +514,10 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     for (hipEvent_t e : poll_ev) (void)hipEventDestroy(e);
     if (!done) {
         // the iteration cap was reached without observing an empty list: verify
-        uint32_t left = 0;
-        HIPCHK(c, hipMemcpy(&left, counts + (fused ? it % 3 : it & 1), 4, hipMemcpyDeviceToHost));
-        if (left != 0) return set_err(c, XRT_ERR_HIP, "iteration cap reached with live paths");
+        uint32_t left[kMaxParts] = {0};
+        HIPCHK(c, hipMemcpy(left, counts_at(fused ? it % 3 : it & 1), P.n_part * 4, hipMemcpyDeviceToHost));
+        for (uint32_t k = 0; k < P.n_part; ++k)
+            if (left[k] != 0) return set_err(c, XRT_ERR_HIP, "iteration cap reached with live paths");
     }
     unsigned long long hs[8] = {0};
     HIPCHK(c, hipMemcpy(hs, P.stats, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
