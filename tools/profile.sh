@@ -15,9 +15,11 @@ B=(python3 "$R/bench.py" --config "$CFG" --steps 1 --warmup 0 --no-cpu --no-timi
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- "${B[@]}" > "$OUT/kt.log" 2>&1
 echo "kernel trace done"
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+    SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS \
     -d "$OUT/sq1" -o sq1 --output-format csv -- "${B[@]}" > "$OUT/sq1.log" 2>&1
 echo "sq1 done"
-timeout -k 10 400 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT \
+timeout -k 10 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR \
+    SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM \
     -d "$OUT/sq2" -o sq2 --output-format csv -- "${B[@]}" > "$OUT/sq2.log" 2>&1
 echo "sq2 done"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- "${B[@]}" > "$OUT/fetch.log" 2>&1

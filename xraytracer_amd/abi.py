@@ -13,6 +13,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libxrt_hip.so")
+if os.environ.get("XRT_LIB"):   # experiment builds (csrc/Makefile `variant`), same ABI
+    LIB_PATH = os.path.join(HERE, os.environ["XRT_LIB"])
 
 XRT_ABI_VERSION = 2   # include/xrt.h XRT_ABI_VERSION
 XRT_OK = 0

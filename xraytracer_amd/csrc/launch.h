@@ -19,7 +19,8 @@ hipError_t launch_shade(const KParams& P, const uint32_t* list, const uint32_t* 
 size_t step_lds_bytes(const KParams& P);
 // up to `visits` path segments per live slot; appends survivors to out (partitioned
 // counters out_count), low-RNG slots to P.req (req_count); clears zero (next-next round)
-hipError_t launch_step(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
+// dP: device copy of P (the triangle-scene kernel reads its parameters from memory)
+hipError_t launch_step(const KParams& P, const KParams* dP, const uint32_t* list, const uint32_t* count, uint32_t* out,
                        uint32_t* out_count, uint32_t* zero, uint32_t* req_count, uint32_t visits, uint32_t blocks,
                        hipStream_t st);
 hipError_t launch_finish(const KParams& P, hipStream_t st);

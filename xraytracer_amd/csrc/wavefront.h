@@ -29,11 +29,11 @@ constexpr uint32_t kRngVisit = 16;   // a slot visit needs at least this many (m
                                      // suspend themselves below 8)
 constexpr uint32_t kMaxParts = 64;   // live-list partitions (counters per list)
 constexpr uint32_t kRefillEvery = 4; // wavefront schedule: k_refill after every 4th k_shade
-constexpr uint32_t kStepVisits = 4;  // fused schedule: path segments per slot per k_step
-constexpr uint32_t kStepRefill = 2;  // fused schedule: k_refill after every 2nd k_step
-constexpr uint32_t kRngKeep = 128;   // fused schedule: a slot queues a refill below this
-                                     // (>= kStepRefill * kStepVisits * 13 + kRngVisit: a
-                                     // GI/Direct slot never waits for words)
+constexpr uint32_t kStepVisits = 32; // fused schedule: path segments per slot per k_step
+constexpr uint32_t kStepRefill = 1;  // fused schedule: k_refill after every k_step
+constexpr uint32_t kVisitDraws = 13; // max RNG draws of one GI/Direct segment (4 lights)
+// fused schedule: a slot queues a refill when fewer than refill * visits * 13 + kRngVisit
+// words are left, so a GI/Direct slot never waits for words (KParams::rng_keep)
 
 // slot state bits
 enum : uint32_t {
@@ -114,6 +114,7 @@ struct KParams {
     int integrator;
     uint32_t max_depth, width, height, spp, shard_index, shard_count, n_slots;
     uint32_t n_part, part_cap;   // live-list partitions: n_part (<= kMaxParts) of part_cap slots
+    uint32_t rng_keep;           // fused schedule refill threshold (words ahead)
     // ---- slot state (SoA)
     f4 *ray_o, *ray_d, *thr, *rad, *thr_prev;
     f4 *hit;     // t, u, v, code(bits)        code: -1 miss, (kind << 28) | prim

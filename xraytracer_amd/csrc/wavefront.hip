@@ -619,6 +619,15 @@ __device__ v3 light_sample(const DLight& L, v3 x, v3& wi, float& pdf, float& tma
 }
 
 // Lambert::sampleDir + uniformSampleHemisphere (Src/material.h:55-73)
+__device__ __forceinline__ v3 lambert_sample_f(v3 ng, v3 dpdu, v3 dpdv, Rng& rng) {
+    const float r1 = rng.next();
+    const float r2 = rng.next();
+    const float sinTheta = __builtin_sqrtf(1.0f - r1 * r1);
+    const float phi = 2.0f * kPI * r2;
+    const float x = sinTheta * glibc_cosf(phi);
+    const float z = sinTheta * glibc_sinf(phi);
+    return local_to_world(mk(x, r1, z), dpdu, ng, dpdv);
+}
 __device__ __forceinline__ v3 lambert_sample(const Surf& S, Rng& rng) {
     const float r1 = rng.next();
     const float r2 = rng.next();
@@ -1099,7 +1108,7 @@ __host__ __device__ inline StepLayout step_layout(const KParams& P) {
 // (step_layout), so this schedule serves scenes up to kStepLds bytes (C1, C2, C3, C5);
 // larger scenes use the multi-pass wavefront (k_shade / k_trace with LDS tiles).  A slot
 // stops early when its RNG ring runs low or it is done; at the end of the launch the slot
-// is appended to the next round's live list and, when fewer than kRngKeep words are left,
+// is appended to the next round's live list and, when fewer than rng_keep words are left,
 // to the refill list k_refill services between rounds.
 struct LScene {
     const f4* tri;      // 3 per triangle
@@ -1113,6 +1122,24 @@ struct LScene {
     const DLight* light;
 };
 
+// Debug instrumentation (-DXRT_COUNT_TESTS, experiment builds only): triangle tests done
+// per lane and per wave (a wave pays for an object when any of its lanes needs it).
+#ifdef XRT_COUNT_TESTS
+#define CNT_PARAM , uint32_t &cnt_l, uint32_t &cnt_w
+#define CNT_ARG , cnt_l, cnt_w
+#define CNT_OBJ(ne, n)                   \
+    do {                                 \
+        if (ne) cnt_l += (n);            \
+        if (__ballot(ne)) cnt_w += (n);  \
+    } while (0)
+#else
+#define CNT_PARAM
+#define CNT_ARG
+#define CNT_OBJ(ne, n) \
+    do {               \
+    } while (0)
+#endif
+
 struct HitRec {
     float t, u, v;
     int code;           // winner: (kind << 28) | index, -1 miss
@@ -1122,14 +1149,16 @@ struct HitRec {
 
 // Scene::intersect over the LDS scene (Src/scene.cpp:190-200)
 template <int SCN>
-__device__ __forceinline__ void closest_l(const KParams& P, const LScene& L, v3 o, v3 d, HitRec& h) {
+__device__ __forceinline__ void closest_l(const KParams& P, const LScene& L, v3 o, v3 d, HitRec& h CNT_PARAM) {
     h.t = kINF, h.u = h.v = 0.0f, h.code = -1, h.surf = -1, h.dp = -1, h.t1 = kINF;
     h.st = h.su = h.sv = h.du = h.dv = 0.0f;
     if (SCN == SCN_TRI) {
         const v3 inv = rcp3(d);
         for (int ob = 0; ob < P.n_objs; ++ob) {
             const DObjBox B = L.box[ob];
-            if (!box_overlap(o, inv, B, h.t)) continue;
+            const bool ne = box_overlap(o, inv, B, h.t);
+            CNT_OBJ(ne, B.count_occ & 0x7fffffff);
+            if (!ne) continue;
             const int end = B.first + (B.count_occ & 0x7fffffff);
             for (int k = B.first; k < end; ++k) {
                 float t, u, v;
@@ -1175,12 +1204,14 @@ __device__ __forceinline__ void closest_l(const KParams& P, const LScene& L, v3 
 
 // Scene::occluded over the LDS scene (Src/scene.cpp:202-211): area-light objects skipped
 template <int SCN>
-__device__ __forceinline__ bool occluded_l(const KParams& P, const LScene& L, v3 o, v3 d, float tmax) {
+__device__ __forceinline__ bool occluded_l(const KParams& P, const LScene& L, v3 o, v3 d, float tmax CNT_PARAM) {
     if (SCN == SCN_TRI) {
         const v3 inv = rcp3(d);
         for (int ob = 0; ob < P.n_objs; ++ob) {
             const DObjBox B = L.box[ob];
-            if (B.count_occ >= 0 || !box_overlap(o, inv, B, tmax)) continue;
+            const bool ne = B.count_occ < 0 && box_overlap(o, inv, B, tmax);
+            CNT_OBJ(ne, B.count_occ & 0x7fffffff);
+            if (!ne) continue;
             const int end = B.first + (B.count_occ & 0x7fffffff);
             for (int k = B.first; k < end; ++k) {
                 float t, u, v;
@@ -1255,8 +1286,11 @@ __device__ __forceinline__ void lds_copy(T* dst, const T* src, int n, int tid) {
     for (int q = tid; q < words; q += kBlock) d[q] = s[q];
 }
 
+#ifndef XRT_STEP_WAVES
+#define XRT_STEP_WAVES 4   // min waves per SIMD the compiler must fit k_step into (<= 128 VGPRs)
+#endif
 template <int SCN, int INTEG>
-__global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __restrict__ list,
+__global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, const uint32_t* __restrict__ list,
                                                   const uint32_t* __restrict__ count, uint32_t* __restrict__ out,
                                                   uint32_t* out_count, uint32_t* zero_count, uint32_t* req_count,
                                                   uint32_t visits) {
@@ -1292,6 +1326,9 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
         const uint32_t s = i < it.n ? list[it.p * P.part_cap + i] : 0;
         uint32_t st = i < it.n ? P.state[s] : ST_DONE;
         bool want_req = false;
+#ifdef XRT_COUNT_TESTS
+        uint32_t cnt_l = 0, cnt_w = 0;
+#endif
         if (!(st & ST_DONE)) {
         const uint32_t g = P.rng_g[s];
         Rng rng{P.ring + (size_t)s * kRing, P.rng_c[s]};
@@ -1305,9 +1342,10 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
         uint32_t nseg = 0, nsh = 0, nrej = 0, nstall = 0;
         const uint32_t col = s % P.width, row = P.shard_index + P.shard_count * (s / P.width);
         float* px = P.fb + 3 * ((size_t)col + (size_t)P.width * row);
+        v3 acc = mk(px[0], px[1], px[2]);   // the pixel's running sum, in registers this launch
+        rng.prefetch(g - rng.c);
         for (uint32_t vis = 0; vis < visits; ++vis) {
             if ((st & ST_DONE) || g - rng.c < kRngVisit) break;
-            rng.prefetch(g - rng.c);
             bool ended = false, trace = true;
             if (st & ST_REGEN) {
                 // next sample: jitter draws + camera ray (Src/renderer.cpp:44-50)
@@ -1333,7 +1371,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
             if (trace) {
                 ++nseg;
                 HitRec h;
-                closest_l<SCN>(P, L, o, d, h);
+                closest_l<SCN>(P, L, o, d, h CNT_ARG);
                 Surf S;
                 const int obj = surface_l<SCN>(L, o, d, h, S);
                 if (INTEG == XRT_INTEGRATOR_DIRECT) {
@@ -1351,7 +1389,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
                             if (pdf == 0.0f) continue;
                             const float bias = 0.01f;
                             ++nsh;
-                            const bool vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias);
+                            const bool vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias CNT_ARG);
                             const float cosv = smax(0.0f, dot(S.ng, wi));
                             const v3 fr = eval_bxdf(ob);
                             rad = rad + (((fr * (float)vis) * Lv) * cosv) / pdf;
@@ -1413,7 +1451,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
                                 if (pdf == 0.0f) continue;
                                 const float bias = 0.01f;
                                 ++nsh;
-                                const bool vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias);
+                                const bool vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias CNT_ARG);
                                 const float cosv = smax(0.0f, dot(S.ng, wi));
                                 const v3 fr = eval_bxdf(ob);
                                 L_light = L_light + (((fr * (float)vis) * Lv) * cosv) / pdf;
@@ -1451,7 +1489,10 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
                     if (depth >= P.max_depth) ended = true;
                 }
             }
-            // finish the sample (Src/renderer.cpp:55-75); the next one starts next segment
+            // finish the sample (Src/renderer.cpp:55-75) and start the next one right away:
+            // its jitter draws are still in the prefetch buffer (a segment draws <= 13 of the
+            // >= 16 words it starts with), so the next segment opens with the trace while
+            // the words it needs next are loading.
             while (ended) {
                 ended = false;
                 const v3 r = rad / 1.0f;
@@ -1459,7 +1500,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
                     __builtin_isinf(r.y) || __builtin_isinf(r.z) || r.x < 0.0f || r.y < 0.0f || r.z < 0.0f) {
                     ++nrej;
                 } else {
-                    px[0] = px[0] + r.x, px[1] = px[1] + r.y, px[2] = px[2] + r.z;
+                    acc = acc + r;
                 }
                 ++k;
                 if (k >= P.spp) {
@@ -1469,12 +1510,18 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
                     rad = mk(0, 0, 0);
                     ended = true;
                 } else {
-                    st |= ST_REGEN;
+                    const float u = ((float)(int)col + rng.next()) / (float)P.width;
+                    const float v = ((float)(int)row + rng.next()) / (float)P.height;
+                    camera_ray(P, u, v, o, d);
+                    thr = mk(1, 1, 1), rad = mk(0, 0, 0);
+                    depth = 0;
                 }
             }
+            rng.prefetch(g - rng.c);
         }
-        // queue an RNG refill for k_refill (Rng words ahead < kRngKeep, once per request)
-        want_req = !(st & (ST_DONE | ST_RNGREQ)) && g - rng.c < kRngKeep;
+        px[0] = acc.x, px[1] = acc.y, px[2] = acc.z;
+        // queue an RNG refill for k_refill (words ahead < rng_keep, once per request)
+        want_req = !(st & (ST_DONE | ST_RNGREQ)) && g - rng.c < P.rng_keep;
         if (want_req) st |= ST_RNGREQ;
         P.state[s] = st;
         if (!(st & (ST_DONE | ST_REGEN))) {
@@ -1491,8 +1538,344 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const uint32_t* __re
         if (nrej) P.c_rej[s] += nrej;
         if (nstall) P.c_stall[s] += nstall;
         }
+#ifdef XRT_COUNT_TESTS
+        {
+            unsigned long long a = cnt_l, b = cnt_w;   // b: per-lane view of the wave's cost
+            for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off);
+            b = b > 0 ? b : 0;
+            unsigned long long bm = b;
+            for (int off = 32; off > 0; off >>= 1) bm = max(bm, (unsigned long long)__shfl_down(bm, off));
+            if (lane == 0) atomicAdd(P.stats + 5, a), atomicAdd(P.stats + 6, bm);
+        }
+#endif
         // live list of the next round and refill requests (partitioned, one atomic per wave)
         wave_append(!(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
+        wave_append(want_req, s, P.req + it.p * P.part_cap, req_count + it.p, lane);
+    }
+}
+
+// ======================================================= cooperative triangle trace ====
+// For triangle scenes the rays of a wave are incoherent after the first bounce: tracing one
+// ray per lane, a wave pays for every object any of its 64 rays needs (measured on C2:
+// ~29 triangle tests per wave per trace while a ray needs ~5).  The cooperative trace
+// instead culls each ray against the object boxes, lays the (ray, triangle) pairs that
+// survive out in one flat index space (exclusive scan over the lanes) and tests 64 pairs
+// per pass — every lane busy.  Results are merged per ray in LDS: closest hit = atomicMin
+// of (t bits << 32 | triangle index), i.e. smallest t and, on a tie, the triangle the
+// reference's in-order `t < best` loop keeps (triangles are packed in Scene iteration
+// order); then the owner lane recomputes u, v of its winner with the same Moller-Trumbore
+// ops.  Shadow rays set an occlusion flag.  Requires n_objs <= 32 (object masks).
+struct CoopWave {
+    f4 ro[64];                     // ray origin, w = tmax (shadow rays)
+    f4 rd[64];
+    unsigned long long best[64];   // closest: packed (t, tri); shadow: != 0 occluded
+    uint32_t pre[64];              // exclusive prefix of the lanes' pair counts
+    uint32_t msk[64];              // objects each ray overlaps
+};
+constexpr int kCoopMaxObjs = 32;
+
+template <bool SHADOW>
+__device__ __forceinline__ unsigned long long coop_trace(const KParams& P, const LScene& L, CoopWave& W, int lane,
+                                                         bool want, v3 o, v3 d, float tmax CNT_PARAM) {
+    uint32_t m = 0, n = 0;
+    if (want) {
+        const v3 inv = rcp3(d);
+        for (int ob = 0; ob < P.n_objs; ++ob) {
+            const DObjBox B = L.box[ob];
+            if (SHADOW && B.count_occ >= 0) continue;   // area-light objects never occlude
+            if (box_overlap(o, inv, B, SHADOW ? tmax : kINF)) m |= 1u << ob, n += B.count_occ & 0x7fffffff;
+        }
+    }
+#ifdef XRT_COUNT_TESTS
+    cnt_l += n;
+#endif
+    uint32_t incl = n;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(incl, off);
+        if (lane >= off) incl += t;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    W.pre[lane] = incl - n;
+    W.msk[lane] = m;
+    W.ro[lane] = make_float4(o.x, o.y, o.z, tmax);
+    W.rd[lane] = make_float4(d.x, d.y, d.z, 0.0f);
+    W.best[lane] = SHADOW ? 0ull : ~0ull;
+    wave_sync();
+#ifdef XRT_COUNT_TESTS
+    cnt_w += (total + 63) / 64 * 64;
+#endif
+    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        if (j < total) {
+            // owner ray: the last lane whose prefix is <= j (it has pairs: see DESIGN.md)
+            int r = 0;
+#pragma unroll
+            for (int step = 32; step > 0; step >>= 1)
+                if (W.pre[r + step] <= j) r += step;
+            uint32_t q = j - W.pre[r], mm = W.msk[r];
+            int ob = __builtin_ctz(mm);
+            uint32_t c = L.box[ob].count_occ & 0x7fffffff;
+            while (q >= c) {
+                q -= c;
+                mm &= mm - 1;
+                ob = __builtin_ctz(mm);
+                c = L.box[ob].count_occ & 0x7fffffff;
+            }
+            const int k = L.box[ob].first + (int)q;
+            const f4 A = W.ro[r];
+            const v3 ro = xyz(A), rd = xyz(W.rd[r]);
+            float t, u, v;
+            if (ray_tri(ro, rd, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t, u, v)) {
+                if (SHADOW) {
+                    if (t < A.w) W.best[r] = 1ull;
+                } else {
+                    atomicMin(&W.best[r], ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)k);
+                }
+            }
+        }
+    }
+    wave_sync();
+    return W.best[lane];
+}
+
+__device__ __forceinline__ void coop_closest(const KParams& P, const LScene& L, CoopWave& W, int lane, bool want, v3 o,
+                                             v3 d, HitRec& h CNT_PARAM) {
+    const unsigned long long b = coop_trace<false>(P, L, W, lane, want, o, d, kINF CNT_ARG);
+    h.t = kINF, h.u = h.v = 0.0f, h.code = -1, h.surf = -1, h.dp = -1, h.t1 = kINF;
+    h.st = h.su = h.sv = h.du = h.dv = 0.0f;
+    if (want && b != ~0ull) {
+        const int k = (int)(uint32_t)b;
+        float t, u, v;
+        (void)ray_tri(o, d, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t, u, v);
+        h.t = t, h.u = u, h.v = v, h.code = k;
+    }
+}
+
+// k_step for triangle scenes (GI / Direct) with cooperative traces: the same per-slot
+// sequence as k_step, arranged so every trace is reached by the whole wave (per-lane
+// activity flags instead of divergent control flow around the traces).
+template <int INTEG>
+__global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KParams* __restrict__ Pp,
+                                                                      const uint32_t* __restrict__ list,
+                                                                      const uint32_t* __restrict__ count,
+                                                                      uint32_t* __restrict__ out, uint32_t* out_count,
+                                                                      uint32_t* zero_count, uint32_t* req_count,
+                                                                      uint32_t visits) {
+    // KParams lives in device memory here (one copy per render): fields are fetched with
+    // scalar loads when needed instead of pinning ~150 SGPRs of kernel arguments
+    const KParams& P = *Pp;
+    extern __shared__ __attribute__((aligned(16))) f4 lds_step[];
+    char* lb = reinterpret_cast<char*>(lds_step);
+    const StepLayout Lo = step_layout(P);
+    LScene L;
+    L.tri = reinterpret_cast<const f4*>(lb + Lo.tri);
+    L.tng = reinterpret_cast<const f4*>(lb + Lo.tng);
+    L.nrm = reinterpret_cast<const f4*>(lb + Lo.nrm);
+    L.box = reinterpret_cast<const DObjBox*>(lb + Lo.box);
+    L.sph = reinterpret_cast<const f4*>(lb + Lo.sph);
+    L.bx = reinterpret_cast<const f4*>(lb + Lo.bx);
+    L.obj = reinterpret_cast<const DObj*>(lb + Lo.obj);
+    L.light = reinterpret_cast<const DLight*>(lb + Lo.light);
+    L.sobj = reinterpret_cast<const int*>(lb + Lo.sobj);
+    const int tid = threadIdx.x, lane = tid & 63;
+    CoopWave& W = reinterpret_cast<CoopWave*>(lb + ((Lo.total + 15u) & ~15u))[tid >> 6];
+    lds_copy(const_cast<f4*>(L.tri), P.tri, 3 * P.n_tris, tid);
+    lds_copy(const_cast<f4*>(L.tng), P.tri_ng, P.n_tris, tid);
+    lds_copy(const_cast<f4*>(L.nrm), P.tri_nrm, 3 * P.n_tris, tid);
+    lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid);
+    lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
+    lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid);
+    __syncthreads();
+    zero_parts(P, zero_count);
+    const PartIter it = part_iter(P, count, kBlock);
+    for (uint32_t base = it.first; base < it.n; base += it.stride) {
+        const uint32_t i = base + tid;
+        const uint32_t s = i < it.n ? list[it.p * P.part_cap + i] : 0;
+        uint32_t st = i < it.n ? P.state[s] : ST_DONE;
+        const bool live = !(st & ST_DONE);
+#ifdef XRT_COUNT_TESTS
+        uint32_t cnt_l = 0, cnt_w = 0;
+#endif
+        uint32_t g = 0, depth = 0, k = 0;
+        Rng rng{P.ring + (size_t)s * kRing, 0};
+        v3 thr = mk(1, 1, 1), rad = mk(0, 0, 0), o = mk(0, 0, 0), d = mk(0, 0, 0), acc = mk(0, 0, 0);
+        const uint32_t col = s % P.width, row = P.shard_index + P.shard_count * (s / P.width);
+        float* px = P.fb + 3 * ((size_t)col + (size_t)P.width * row);
+        if (live) {
+            g = P.rng_g[s];
+            rng.c = P.rng_c[s];
+            depth = P.depth[s];
+            k = P.sample_k[s];
+            if (!(st & ST_REGEN)) {
+                thr = xyz(P.thr[s]), rad = xyz(P.rad[s]);
+                o = xyz(P.ray_o[s]), d = xyz(P.ray_d[s]);
+            }
+            acc = mk(px[0], px[1], px[2]);
+            rng.prefetch(g - rng.c);
+        }
+        uint32_t nseg = 0, nsh = 0, nrej = 0;
+        for (uint32_t vis = 0; vis < visits; ++vis) {
+            const bool act = live && !(st & ST_DONE) && g - rng.c >= kRngVisit;
+            if (!__ballot(act)) break;
+            if (act && (st & ST_REGEN)) {
+                // first sample of the slot: jitter draws + camera ray (Src/renderer.cpp:44-50)
+                st &= ~ST_REGEN;
+                const float u = ((float)(int)col + rng.next()) / (float)P.width;
+                const float v = ((float)(int)row + rng.next()) / (float)P.height;
+                camera_ray(P, u, v, o, d);
+                thr = mk(1, 1, 1), rad = mk(0, 0, 0);
+                depth = 0;
+            }
+            bool ended = false, alive = false;
+            if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) ended = act;   // bounce loop never runs
+            const bool ext = act && !ended;
+            HitRec h;
+            coop_closest(P, L, W, lane, ext, o, d, h CNT_ARG);
+            // SurfaceInfo of a triangle hit: position, face normal; the shading normal (for
+            // Le) and the dpdu/dpdv frame (for the BSDF) are rebuilt from (tri, u, v) where used
+            Surf S;
+            S.pos = S.ng = S.ns = S.dpdu = S.dpdv = mk(0, 0, 0);
+            int obj = -1;
+            const int hk = h.code;
+            const float hu = h.u, hv = h.v;
+            if (ext) {
+                ++nseg;
+                if (hk >= 0) {
+                    S.pos = ray_at(o, d, h.t);
+                    S.ng = xyz(L.tng[hk]);
+                    obj = __float_as_int(L.tri[3 * hk].w);
+                }
+                if (INTEG == XRT_INTEGRATOR_DIRECT) {
+                    // DirectIntegrator::integrate (Src/integrator.h:82-119)
+                    if (obj < 0) {
+                        rad = mk((float)0.18, (float)0.18, (float)0.18);
+                        ended = true;
+                    } else if (L.obj[obj].light >= 0) {
+                        rad = light_Le(L.light[L.obj[obj].light], tri_ns_l(L, hk, hu, hv), d);
+                        ended = true;
+                    } else {
+                        alive = true;
+                    }
+                } else {
+                    // GIIntegrator::integrate loop body (Src/integrator.h:214-284)
+                    if (obj < 0) {
+                        rad = rad + thr * mk(0.0f, 0.0f, 0.0f);
+                        ended = true;
+                    } else {
+                        alive = true;
+                        if (depth > 0) {
+                            const float pr = smin((thr.x + thr.y + thr.z) / 3.0f, 1.0f);
+                            if (rng.next() >= pr) alive = false, ended = true;
+                            else thr = thr / mk(pr, pr, pr);
+                        }
+                        if (alive && L.obj[obj].light >= 0) {
+                            if (depth == 0)
+                                rad = rad + thr * light_Le(L.light[L.obj[obj].light], tri_ns_l(L, hk, hu, hv), d);
+                            alive = false, ended = true;
+                        }
+                    }
+                }
+            }
+            // next-event estimation: one cooperative shadow trace per light, in light order
+            v3 directL = mk(0, 0, 0);
+            for (int l = 0; l < P.n_lights; ++l) {
+                v3 wi = mk(0, 0, 0), Lv = mk(0, 0, 0);
+                float tmax = 0.0f, pdf = 0.0f;
+                if (alive) Lv = light_sample(L.light[l], S.pos, wi, pdf, tmax, rng);
+                const bool sh = alive && pdf != 0.0f;
+                const float bias = 0.01f;
+                const bool occ = coop_trace<true>(P, L, W, lane, sh, S.pos + S.ng * bias, wi, tmax - bias CNT_ARG) != 0;
+                if (sh) {
+                    ++nsh;
+                    const float cosv = smax(0.0f, dot(S.ng, wi));
+                    const v3 fr = eval_bxdf(L.obj[obj]);
+                    const v3 c = (((fr * (float)!occ) * Lv) * cosv) / pdf;
+                    if (INTEG == XRT_INTEGRATOR_DIRECT) {
+                        rad = rad + c;
+                    } else {
+                        const v3 L_light = mk(0, 0, 0) + c;
+                        directL = directL + L_light;
+                    }
+                }
+            }
+            if (alive) {
+                if (INTEG == XRT_INTEGRATOR_DIRECT) {
+                    ended = true;
+                } else {
+                    rad = rad + thr * directL;
+                    const DObj& ob = L.obj[obj];
+                    float pdf = 1.0f;
+                    v3 nd = mk(0, 0, 0), fr = mk(0, 0, 0);
+                    if (ob.material == 1) {
+                        v3 dpdu, dpdv;
+                        onb(tri_ns_l(L, hk, hu, hv), dpdu, dpdv);
+                        nd = lambert_sample_f(S.ng, dpdu, dpdv, rng);
+                        pdf = 1.0f / (2.0f * kPI);
+                        fr = eval_bxdf(ob);
+                    }
+                    const float cosv = smax(0.0f, dot(nd, S.ng));
+                    thr = thr * ((fr * cosv) / pdf);
+                    o = S.pos + S.ng * 0.01f;
+                    d = nd;
+                    ++depth;
+                    if (depth >= P.max_depth) ended = true;
+                }
+            }
+            // finish the sample and start the next one (see k_step)
+            while (ended) {
+                ended = false;
+                const v3 r = rad / 1.0f;
+                if (__builtin_isnan(r.x) || __builtin_isnan(r.y) || __builtin_isnan(r.z) || __builtin_isinf(r.x) ||
+                    __builtin_isinf(r.y) || __builtin_isinf(r.z) || r.x < 0.0f || r.y < 0.0f || r.z < 0.0f) {
+                    ++nrej;
+                } else {
+                    acc = acc + r;
+                }
+                ++k;
+                if (k >= P.spp) {
+                    st = ST_DONE;
+                } else if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) {
+                    (void)rng.next(), (void)rng.next();
+                    rad = mk(0, 0, 0);
+                    ended = true;
+                } else {
+                    const float u = ((float)(int)col + rng.next()) / (float)P.width;
+                    const float v = ((float)(int)row + rng.next()) / (float)P.height;
+                    camera_ray(P, u, v, o, d);
+                    thr = mk(1, 1, 1), rad = mk(0, 0, 0);
+                    depth = 0;
+                }
+            }
+            if (act) rng.prefetch(g - rng.c);
+        }
+        bool want_req = false;
+        if (live) {
+            px[0] = acc.x, px[1] = acc.y, px[2] = acc.z;
+            want_req = !(st & (ST_DONE | ST_RNGREQ)) && g - rng.c < P.rng_keep;
+            if (want_req) st |= ST_RNGREQ;
+            P.state[s] = st;
+            if (!(st & (ST_DONE | ST_REGEN))) {
+                P.depth[s] = depth;
+                P.thr[s] = pk(thr);
+                P.rad[s] = pk(rad);
+                P.ray_o[s] = pk(o);
+                P.ray_d[s] = pk(d);
+            }
+            P.sample_k[s] = k;
+            P.rng_c[s] = rng.c;
+            if (nseg) P.c_seg[s] += nseg;
+            if (nsh) P.c_shadow[s] += nsh;
+            if (nrej) P.c_rej[s] += nrej;
+        }
+#ifdef XRT_COUNT_TESTS
+        {
+            unsigned long long a = cnt_l, b = cnt_w;
+            for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off);
+            if (lane == 0) atomicAdd(P.stats + 5, a), atomicAdd(P.stats + 6, b / 64);
+        }
+#endif
+        wave_append(live && !(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
         wave_append(want_req, s, P.req + it.p * P.part_cap, req_count + it.p, lane);
     }
 }
@@ -1689,10 +2072,26 @@ static hipError_t step_i(const KParams& P, const uint32_t* list, const uint32_t*
     return hipGetLastError();
 }
 
-hipError_t launch_step(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
+static bool use_step_tri(const KParams& P) {
+    return P.scene_kind == SCN_TRI && P.small_tri && P.n_objs <= kCoopMaxObjs &&
+           P.integrator != XRT_INTEGRATOR_VPT && !std::getenv("XRT_NO_COOP") &&
+           ((step_layout(P).total + 15u) & ~15u) + (kBlock / 64) * sizeof(CoopWave) <= kStepLds;
+}
+
+hipError_t launch_step(const KParams& P, const KParams* dP, const uint32_t* list, const uint32_t* count, uint32_t* out,
                        uint32_t* out_count, uint32_t* zero, uint32_t* req_count, uint32_t visits, uint32_t blocks,
                        hipStream_t st) {
     if (!step_lds_bytes(P)) return hipErrorInvalidValue;
+    if (use_step_tri(P)) {
+        const size_t lds = ((step_layout(P).total + 15u) & ~15u) + (kBlock / 64) * sizeof(CoopWave);
+        if (P.integrator == XRT_INTEGRATOR_DIRECT)
+            hipLaunchKernelGGL((k_step_tri<XRT_INTEGRATOR_DIRECT>), dim3(blocks), dim3(kBlock), lds, st, dP, list,
+                               count, out, out_count, zero, req_count, visits);
+        else
+            hipLaunchKernelGGL((k_step_tri<XRT_INTEGRATOR_GI>), dim3(blocks), dim3(kBlock), lds, st, dP, list, count,
+                               out, out_count, zero, req_count, visits);
+        return hipGetLastError();
+    }
     switch (P.scene_kind) {
         case SCN_TRI: return step_i<SCN_TRI>(P, list, count, out, out_count, zero, req_count, visits, blocks, st);
         case SCN_SPHERE: return step_i<SCN_SPHERE>(P, list, count, out, out_count, zero, req_count, visits, blocks, st);

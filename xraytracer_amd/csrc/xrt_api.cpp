@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -40,7 +41,7 @@ struct xrt_ctx {
     size_t cap_slots = 0;
     DevBuf ray_o, ray_d, thr, rad, thr_prev, hit, hit2, hit3, sh_o, sh_d, sh_c, med, med2;
     DevBuf state, sample_k, depth, occ, rng_c, rng_g, ring, c_seg, c_shadow, c_rej, c_stall, lists;
-    DevBuf counts, stats, fb, scratch;
+    DevBuf counts, stats, fb, scratch, kparams;
     size_t cap_fb = 0;
     uint32_t* h_poll = nullptr;  // pinned
     std::vector<hipEvent_t> events;
@@ -96,6 +97,13 @@ T* as(DevBuf& b) {
 
 uint32_t shard_rows(uint32_t h, uint32_t idx, uint32_t n) { return idx < h ? (h - idx + n - 1) / n : 0; }
 
+uint32_t env_u32(const char* name, uint32_t dflt, uint32_t lo, uint32_t hi) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    const long x = std::strtol(v, nullptr, 10);
+    return (uint32_t)std::min<long>(hi, std::max<long>(lo, x));
+}
+
 }  // namespace
 
 extern "C" {
@@ -127,7 +135,7 @@ void xrt_destroy(xrt_ctx* c) {
                      &c->segs, &c->density, &c->obj_box, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
                      &c->hit2, &c->hit3, &c->sh_o, &c->sh_d, &c->sh_c, &c->med, &c->med2, &c->state,
                      &c->sample_k, &c->depth, &c->occ, &c->rng_c, &c->rng_g, &c->ring, &c->c_seg, &c->c_shadow,
-                     &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch};
+                     &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch, &c->kparams};
     for (DevBuf* b : all) free_buf(*b);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     if (c->h_poll) (void)hipHostFree(c->h_poll);
@@ -456,6 +464,16 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     // iterations).  k_step rotates three live counters: round i reads counts[i%3], appends
     // to counts[(i+1)%3] and clears counts[(i+2)%3] for round i+1.
     const bool fused = !(p->flags & XRT_FLAG_WAVEFRONT) && step_lds_bytes(P) != 0;
+    // tuning knobs (defaults kStepVisits / kStepRefill; XRT_STEP_VISITS / XRT_STEP_REFILL
+    // override them for experiments — results do not depend on them)
+    const uint32_t step_visits = env_u32("XRT_STEP_VISITS", kStepVisits, 1, 64);
+    const uint32_t step_refill = env_u32("XRT_STEP_REFILL", kStepRefill, 1, 8);
+    P.rng_keep = step_refill * step_visits * kVisitDraws + kRngVisit;
+    if (P.rng_keep > kMT) return set_err(c, XRT_ERR_INVALID, "XRT_STEP_VISITS * XRT_STEP_REFILL too large");
+    // device copy of the (now final) parameters for kernels that read them from memory
+    if ((rc = ensure(c, c->kparams, sizeof(KParams)))) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->kparams.p, &P, sizeof(KParams), hipMemcpyHostToDevice, c->stream));
+    const KParams* dP = as<KParams>(c->kparams);
     const uint64_t poll_every = fused ? 4 : kPoll, ahead = fused ? 16 : kAhead;
     for (; it < cap_iters && !done; ++it) {
         const int cur = (int)(it & 1), nxt = cur ^ 1;
@@ -464,11 +482,11 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             const int ci = (int)(it % 3), co = (int)((it + 1) % 3), cz = (int)((it + 2) % 3);
             live = counts_at(co);
             hipError_t e = launch(XRT_K_STEP, [&] {
-                return launch_step(P, lists[cur], counts_at(ci), lists[nxt], counts_at(co), counts_at(cz),
-                                   req_counts + (epoch & 1) * kMaxParts, kStepVisits, blocks, c->stream);
+                return launch_step(P, dP, lists[cur], counts_at(ci), lists[nxt], counts_at(co), counts_at(cz),
+                                   req_counts + (epoch & 1) * kMaxParts, step_visits, blocks, c->stream);
             });
             if (e != hipSuccess) return hip_err(c, e, "k_step");
-            if (it % kStepRefill == kStepRefill - 1) {
+            if (it % step_refill == step_refill - 1) {
                 e = refill();
                 if (e != hipSuccess) return hip_err(c, e, "k_refill");
             }
@@ -520,7 +538,8 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             if (left[k] != 0) return set_err(c, XRT_ERR_HIP, "iteration cap reached with live paths");
     }
     unsigned long long hs[8] = {0};
-    HIPCHK(c, hipMemcpy(hs, P.stats, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(hs, P.stats, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (hs[5] || hs[6]) std::fprintf(stderr, "[xrt] triangle tests: lane %llu wave %llu\n", hs[5], hs[6]);
     S.segments = hs[0], S.shadow_rays = hs[1], S.draws = hs[2], S.rejected = hs[3], S.stalled = hs[4];
     if (timing) {
         for (auto& u : ev_use) {
