@@ -1559,8 +1559,8 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
 // ray per lane, a wave pays for every object any of its 64 rays needs (measured on C2:
 // ~29 triangle tests per wave per trace while a ray needs ~5).  The cooperative trace
 // instead culls each ray against the object boxes, lays the (ray, triangle) pairs that
-// survive out in one flat index space (exclusive scan over the lanes) and tests 64 pairs
-// per pass — every lane busy.  Results are merged per ray in LDS: closest hit = atomicMin
+// survive out in one flat index space (exclusive scan over the lanes; each lane writes its
+// pairs into an LDS list, 512 per chunk) and tests 64 pairs per pass — every lane busy.  Results are merged per ray in LDS: closest hit = atomicMin
 // of (t bits << 32 | triangle index), i.e. smallest t and, on a tie, the triangle the
 // reference's in-order `t < best` loop keeps (triangles are packed in Scene iteration
 // order); then the owner lane recomputes u, v of its winner with the same Moller-Trumbore
@@ -1569,10 +1569,10 @@ struct CoopWave {
     f4 ro[64];                     // ray origin, w = tmax (shadow rays)
     f4 rd[64];
     unsigned long long best[64];   // closest: packed (t, tri); shadow: != 0 occluded
-    uint32_t pre[64];              // exclusive prefix of the lanes' pair counts
-    uint32_t msk[64];              // objects each ray overlaps
+    uint32_t pair[512];            // expanded pairs of the current chunk: owner << 24 | tri
 };
 constexpr int kCoopMaxObjs = 32;
+constexpr uint32_t kCoopCap = 512;
 
 template <bool SHADOW>
 __device__ __forceinline__ unsigned long long coop_trace(const KParams& P, const LScene& L, CoopWave& W, int lane,
@@ -1596,37 +1596,36 @@ __device__ __forceinline__ unsigned long long coop_trace(const KParams& P, const
         if (lane >= off) incl += t;
     }
     const uint32_t total = __shfl(incl, 63);
-    W.pre[lane] = incl - n;
-    W.msk[lane] = m;
+    const uint32_t pre = incl - n;
     W.ro[lane] = make_float4(o.x, o.y, o.z, tmax);
     W.rd[lane] = make_float4(d.x, d.y, d.z, 0.0f);
     W.best[lane] = SHADOW ? 0ull : ~0ull;
-    wave_sync();
 #ifdef XRT_COUNT_TESTS
     cnt_w += (total + 63) / 64 * 64;
 #endif
-    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
-        const uint32_t j = j0 + lane;
-        if (j < total) {
-            // owner ray: the last lane whose prefix is <= j (it has pairs: see DESIGN.md)
-            int r = 0;
-#pragma unroll
-            for (int step = 32; step > 0; step >>= 1)
-                if (W.pre[r + step] <= j) r += step;
-            uint32_t q = j - W.pre[r], mm = W.msk[r];
-            int ob = __builtin_ctz(mm);
-            uint32_t c = L.box[ob].count_occ & 0x7fffffff;
-            while (q >= c) {
-                q -= c;
+    for (uint32_t c0 = 0; c0 < total; c0 += kCoopCap) {
+        // expand this lane's pairs that fall into the chunk [c0, c0 + kCoopCap)
+        if (n && pre < c0 + kCoopCap && pre + n > c0) {
+            uint32_t pos = pre, mm = m;
+            while (mm) {
+                const int ob = __builtin_ctz(mm);
                 mm &= mm - 1;
-                ob = __builtin_ctz(mm);
-                c = L.box[ob].count_occ & 0x7fffffff;
+                const DObjBox B = L.box[ob];
+                const uint32_t c = B.count_occ & 0x7fffffff;
+                const uint32_t lo = max(pos, c0), hi = min(pos + c, c0 + kCoopCap);
+                for (uint32_t q = lo; q < hi; ++q) W.pair[q - c0] = ((uint32_t)lane << 24) | (B.first + (q - pos));
+                pos += c;
             }
-            const int k = L.box[ob].first + (int)q;
+        }
+        wave_sync();
+        const uint32_t cnt = min(kCoopCap, total - c0);
+        for (uint32_t j = lane; j < cnt; j += 64) {
+            const uint32_t e = W.pair[j];
+            const int r = (int)(e >> 24), k = (int)(e & 0xffffffu);
             const f4 A = W.ro[r];
-            const v3 ro = xyz(A), rd = xyz(W.rd[r]);
             float t, u, v;
-            if (ray_tri(ro, rd, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t, u, v)) {
+            if (ray_tri(xyz(A), xyz(W.rd[r]), xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t, u,
+                        v)) {
                 if (SHADOW) {
                     if (t < A.w) W.best[r] = 1ull;
                 } else {
@@ -1634,8 +1633,8 @@ __device__ __forceinline__ unsigned long long coop_trace(const KParams& P, const
                 }
             }
         }
+        wave_sync();
     }
-    wave_sync();
     return W.best[lane];
 }
 
