@@ -21,23 +21,18 @@ METRIC = "Msamples/s (whole node) + wall-clock at 800×600×1024spp, 1/2/4/8 MI3
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3        # vector FP32 spec
 
-# Algorithmic bytes per unit of work, from the data layout in DESIGN.md §Roofline:
-#   k_trace : per extension ray  — list 4 + state 4 + ray o,d 32 + hit record 16         = 56
-#             per shadow ray     — shadow o+tmax, d 32 + occlusion word 4                  = 36
-#   k_shade : per slot visit     — list 4 + state 4+4 + depth/k 8+8 + thr,rad 32+32
-#                                  + rng cursor/gen 8+8 + list out 4                       = 112
-#             per traced hit     — hit 16 + ray o,d 32 read + 32 write                     = 80
-#             per shadow ray     — record write o,d,contrib 48 + thr_prev 16 + read back
-#                                  contrib 16 + occlusion 4                                = 84
-#             per RNG draw       — 4 (tempered word) + 8 (amortised twist: 2*2496 B / 624) = 12
-#             per sample         — framebuffer read-modify-write 24
-#   k_step  : per segment        — list 4 + state 4+4 + depth/k 8+8 + thr,rad 32+32
-#                                  + ray o,d 32+32 + rng cursor/gen 8+8 + list out 4       = 176
-#             (+ per RNG draw 12, per sample 24 as above; the scene is read from LDS)
-B_TRACE_RAY, B_TRACE_SHADOW = 56, 36
-B_SHADE_VISIT, B_SHADE_HIT, B_SHADE_SHADOW, B_DRAW, B_SAMPLE = 112, 80, 84, 12, 24
-B_STEP_SEG = 176
-FLOP_PER_TRI_TEST = 40          # Moller-Trumbore with one correctly-rounded divide, approx.
+# Roofline model: algorithmic bytes per sample of the
+# path, B_s = 68 + 264·Q + 12·D, with Q = extension segments per sample and D = RNG draws
+# per sample (both counted by the device and identical to the CPU restatement's counts):
+#   68  per sample  — 44 B generated ray (o, d, thr, pixel, depth) + 24 B accumulate RMW
+#   264 per segment — extend (o,d read 24 + hit write 16), shade (read 44 + 16, write next
+#                     ray 44 + shadow ray 44), shadow (read 44 + RMW 24), compaction 8
+#   12  per draw    — 4 B tempered word + 8 B amortised twist (2 * 2496 B / 624)
+# The fused schedule (k_step / k_step_tri) performs all of it in one kernel; the wavefront
+# schedule splits it: k_trace = extend + shadow (108·Q), k_shade = the rest.
+B_SAMPLE, B_SEGMENT, B_DRAW = 68, 264, 12
+B_TRACE_SEG = 24 + 16 + 44 + 24
+FLOP_PER_TRI_TEST = 40          # Moller-Trumbore arithmetic per triangle test (secondary)
 
 
 def env_int(k, d):
@@ -71,7 +66,7 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--spp", type=int, default=None, help="override spp (never for reported numbers)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-spp", type=int, default=32)
+    ap.add_argument("--cpu-spp", type=int, default=256)
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--schedule", default="auto", choices=("auto", "wavefront"))
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
@@ -126,6 +121,7 @@ def main():
         for k in agg:
             agg[k] += getattr(st, k)
         kms += np.array(list(st.kernel_ms))
+        sched = int(st.schedule)
         kl += np.array(list(st.launches))
     torch.cuda.synchronize()
     if dist is not None:
@@ -146,40 +142,50 @@ def main():
         # roofline of the dominant kernel (per-launch algorithmic bytes / avg launch time)
         roof = None
         if timing and kms.sum() > 0:
-            bytes_k = {
-                abi.XRT_K_TRACE: B_TRACE_RAY * agg["segments"] + B_TRACE_SHADOW * agg["shadow_rays"],
-                abi.XRT_K_SHADE: (B_SHADE_VISIT * (agg["segments"] + agg["samples"] / max(1, world))
-                                  + B_SHADE_HIT * agg["segments"] + B_SHADE_SHADOW * agg["shadow_rays"]
-                                  + B_DRAW * agg["draws"] + B_SAMPLE * agg["samples"]),
-                abi.XRT_K_STEP: B_STEP_SEG * agg["segments"] + B_DRAW * agg["draws"] + B_SAMPLE * agg["samples"],
-            }
-            if world > 1:   # per-rank kernel times, whole-job counters: use rank-0 share
-                bytes_k = {k: v / world for k, v in bytes_k.items()}
+            samples = agg["samples"] / max(1, world)            # this rank's share
+            q = agg["segments"] / max(1, agg["samples"])
+            dpp = agg["draws"] / max(1, agg["samples"])
+            b_s = B_SAMPLE + B_SEGMENT * q + B_DRAW * dpp
             dom = max((abi.XRT_K_TRACE, abi.XRT_K_SHADE, abi.XRT_K_STEP), key=lambda k: kms[k])
-            per_launch_bytes = bytes_k[dom] / max(1, kl[dom])
-            avg_s = kms[dom] / 1e3 / max(1, kl[dom])
-            achieved = per_launch_bytes / avg_s / 1e9
+            if dom == abi.XRT_K_STEP:
+                kbytes = b_s * samples
+            elif dom == abi.XRT_K_TRACE:
+                kbytes = B_TRACE_SEG * q * samples
+            else:
+                kbytes = (b_s - B_TRACE_SEG * q) * samples
+            launches = max(1, kl[dom])
+            per_launch = kbytes / launches
+            avg_s = kms[dom] / 1e3 / launches
+            achieved = per_launch / avg_s / 1e9
+            kname = abi.KERNEL_NAMES[dom]
+            if dom == abi.XRT_K_STEP and sched == abi.XRT_SCHED_STEP_TRI:
+                kname = "step_tri"
             traffic = None
             if os.path.exists(args.traffic):
                 try:
                     tj = json.load(open(args.traffic))
-                    if tj.get("config") == args.config:
-                        traffic = tj.get("per_launch_bytes", {}).get(abi.KERNEL_NAMES[dom])
+                    if tj.get("config") == args.config and tj.get("kernel") == "k_" + kname:
+                        traffic = tj.get("hbm_bytes_per_launch")
                 except (OSError, ValueError):
                     traffic = None
-            roof = {"bound": "hbm", "kernel": "k_" + abi.KERNEL_NAMES[dom], "achieved": round(achieved, 2),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                    "traffic": traffic, "avg_launch_us": round(avg_s * 1e6, 3),
-                    "launches": int(kl[dom]), "algorithmic_bytes_per_launch": round(per_launch_bytes, 1)}
-            tri_tests = 0
-            if scene.desc.n_tris:
-                tri_tests = scene.desc.n_tris * (agg["segments"] + agg["shadow_rays"])   # upper bound
-            tk = abi.XRT_K_STEP if kl[abi.XRT_K_STEP] else abi.XRT_K_TRACE
-            if tri_tests and kms[tk] > 0:
-                roof["valu_tflops_trace_upper"] = round(
-                    tri_tests * FLOP_PER_TRI_TEST / (kms[tk] / 1e3) / 1e12 / max(1, world), 3)
+            roof = {"bound": "hbm", "kernel": "k_" + kname, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                    "avg_launch_us": round(avg_s * 1e6, 3), "launches": int(kl[dom]),
+                    "algorithmic_bytes_per_launch": round(per_launch, 1),
+                    "bytes_per_sample": round(b_s, 2), "model": "SURVEY.md 8d: B_s = 68 + 264*Q + 12*D"}
+            # secondary: the reference's brute-force triangle tests (every object, every
+            # triangle; shadow rays skip area-light objects) x FLOP_PER_TRI_TEST
+            d = scene.desc
+            n_occ = sum(d.objects[i].count for i in range(d.n_objects)
+                        if d.objects[i].kind == abi.XRT_OBJ_MESH and d.objects[i].light < 0)
+            tests = (agg["segments"] * d.n_tris + agg["shadow_rays"] * n_occ) / max(1, world)
+            if tests:
+                tf = tests * FLOP_PER_TRI_TEST / (kms[dom] / 1e3) / 1e12
+                roof["valu"] = {"tri_tests_per_sample": round(tests / max(1, samples), 2),
+                                "achieved_tflops": round(tf, 3), "peak_tflops": FP32_PEAK_TFLOPS,
+                                "frac": round(tf / FP32_PEAK_TFLOPS, 4)}
             roof["kernel_ms_per_step"] = {abi.KERNEL_NAMES[i]: round(kms[i] / args.steps, 3)
-                                          for i in range(abi.XRT_K_COUNT)}
+                                          for i in range(abi.XRT_K_COUNT) if kms[i]}
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
@@ -192,7 +198,8 @@ def main():
                        "segments_per_sample": round(agg["segments"] / max(1, agg["samples"]), 4),
                        "draws_per_sample": round(agg["draws"] / max(1, agg["samples"]), 4),
                        "iterations_per_frame": round(agg["iterations"] / args.steps, 1),
-                       "schedule": "fused k_step" if kl[abi.XRT_K_STEP] else "wavefront k_shade+k_trace"},
+                       "schedule": abi.SCHEDULE_NAMES[sched],
+                       "shadow_rays_per_sample": round(agg["shadow_rays"] / max(1, agg["samples"]), 4)},
             "roofline": roof,
             "cpu_baseline": None,
         }

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 2
+#define XRT_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------------------- */
 enum {
@@ -124,6 +124,10 @@ enum {
     XRT_K_COUNT = 6
 };
 
+/* device schedules: multi-pass wavefront (k_shade + k_trace), fused per-slot k_step with
+ * the scene in LDS, and its triangle-scene form with cooperative (ray, triangle) traces */
+enum { XRT_SCHED_WAVEFRONT = 0, XRT_SCHED_STEP = 1, XRT_SCHED_STEP_TRI = 2 };
+
 typedef struct {
     double wall_ms;              /* host wall clock of the render call (upload excluded) */
     double kernel_ms[XRT_K_COUNT];   /* summed HIP-event time per kernel (XRT_FLAG_TIMING) */
@@ -135,7 +139,7 @@ typedef struct {
     uint64_t rejected;           /* samples dropped by the NaN/Inf/negative check          */
     uint64_t iterations;         /* trace+shade pass pairs, or k_step rounds               */
     uint64_t path_slots;         /* slots in flight (pixels of this shard)                 */
-    uint64_t trace_slot_visits;  /* sum over trace launches of active slots                */
+    uint64_t schedule;           /* XRT_SCHED_* the render ran                             */
     uint64_t stalled;            /* paths stopped by the VPT no-progress guard             */
 } xrt_stats;
 

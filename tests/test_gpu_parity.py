@@ -152,6 +152,7 @@ def test_c1_cornell_gi_bit_exact(renderer, sched):
     compare(img, ref)
     g = renderer.stats
     assert (g.launches[abi.XRT_K_STEP] > 0) == (sched == "auto")
+    assert g.schedule == (abi.XRT_SCHED_STEP_TRI if sched == "auto" else abi.XRT_SCHED_WAVEFRONT)
     assert (g.segments, g.shadow_rays, g.draws, g.rejected) == (st["segments"], st["shadow_rays"], st["draws"],
                                                                 st["rejected"])
 
@@ -206,6 +207,7 @@ def test_c3_spheres_direct(renderer, sched):
     s = scenes.spheres(160, 90)
     img, ref, st = render_both(renderer, s, 160, 90, 4, schedule=sched)
     compare(img, ref)
+    assert renderer.stats.schedule == (abi.XRT_SCHED_STEP if sched == "auto" else abi.XRT_SCHED_WAVEFRONT)
     assert renderer.stats.shadow_rays == st["shadow_rays"]
 
 
@@ -215,6 +217,7 @@ def test_c4_sphere_mesh_gi(renderer):
     img, ref, _ = render_both(renderer, s, 64, 36, 4)
     compare(img, ref)
     assert renderer.stats.launches[abi.XRT_K_STEP] == 0   # too large for LDS: multi-pass schedule
+    assert renderer.stats.schedule == abi.XRT_SCHED_WAVEFRONT
 
 
 def test_triangle_light_and_two_lights(renderer, sched):

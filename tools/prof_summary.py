@@ -1,27 +1,45 @@
-"""tools/prof_summary.py DIR [kernel-substring] — summarise a tools/profile.sh run: per-kernel
-time from the kernel trace, and summed PMC counters of the chosen kernel with derived
-ratios (lane utilisation, wait fractions, bytes)."""
+"""tools/prof_summary.py DIR [kernel-substring] [--traffic CONFIG OUT.json] — summarise a
+tools/profile.sh run: per-kernel time from the kernel trace, summed PMC counters of the
+chosen kernel with derived ratios, and (with --traffic) the per-launch HBM bytes of that
+kernel for bench.py's roofline.traffic, corrected as MI355X_MICROARCH.md §HBM prescribes:
+FETCH_SIZE (KiB) doubled on gfx950, WRITE_SIZE (KiB) as is, each from its own pass."""
 import collections
 import csv
 import glob
+import json
 import os
+import re
 import sys
 
 
 def main():
-    d = sys.argv[1]
-    pat = sys.argv[2] if len(sys.argv) > 2 else "k_step"
+    args = sys.argv[1:]
+    traffic = None
+    if "--traffic" in args:
+        i = args.index("--traffic")
+        traffic = (args[i + 1], args[i + 2])
+        del args[i:i + 3]
+    d = args[0]
+    pat = args[1] if len(args) > 1 else "k_step"
     st = glob.glob(os.path.join(d, "kt", "*kernel_stats.csv"))
+    avg_ns = None
     if st:
         for r in csv.DictReader(open(st[0])):
-            print(f'{float(r["TotalDurationNs"]) / 1e6:9.3f} ms {int(r["Calls"]):6d} calls  {r["Name"][:90]}')
+            print(f'{float(r["TotalDurationNs"]) / 1e6:9.3f} ms {int(r["Calls"]):6d} calls '
+                  f'avg {float(r["AverageNs"]) / 1e3:9.2f} us  {r["Name"][:80]}')
+            if pat in r["Name"] and avg_ns is None:
+                avg_ns = float(r["AverageNs"])
     acc = collections.defaultdict(float)
     n = collections.Counter()
+    kname = None
     for f in glob.glob(os.path.join(d, "*", "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             if pat in r["Kernel_Name"]:
                 acc[r["Counter_Name"]] += float(r["Counter_Value"])
                 n[r["Counter_Name"]] += 1
+                if kname is None:
+                    m = re.search(r"(k_\w+)", r["Kernel_Name"])
+                    kname = m.group(1) if m else pat
     for k in sorted(acc):
         print(f"{k:28s} {acc[k]:.4g}  ({n[k]} dispatches)")
     a = acc
@@ -34,10 +52,21 @@ def main():
                   "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_LDS"):
             if k in a:
                 print(f"{k:28s} / WAVE_CYCLES = {a[k] / w:.3f}")
-    if a.get("FETCH_SIZE") is not None and "FETCH_SIZE" in a:
-        print("FETCH_SIZE x2 (gfx950 correction) = %.3f GB" % (2 * a["FETCH_SIZE"] * 1024 / 1e9))
-    if "WRITE_SIZE" in a:
-        print("WRITE_SIZE = %.3f GB" % (a["WRITE_SIZE"] * 1024 / 1e9))
+    fetch = 2 * a["FETCH_SIZE"] * 1024 if "FETCH_SIZE" in a else None
+    write = a["WRITE_SIZE"] * 1024 if "WRITE_SIZE" in a else None
+    if fetch is not None:
+        print("FETCH_SIZE x2 (gfx950 correction) = %.3f GB" % (fetch / 1e9))
+    if write is not None:
+        print("WRITE_SIZE = %.3f GB" % (write / 1e9))
+    if traffic and fetch is not None and write is not None:
+        launches = n["FETCH_SIZE"]
+        out = {"config": traffic[0], "kernel": kname, "launches": launches,
+               "fetch_bytes_per_launch": fetch / launches, "write_bytes_per_launch": write / launches,
+               "hbm_bytes_per_launch": (fetch + write) / launches,
+               "avg_launch_us_rocprof": avg_ns / 1e3 if avg_ns else None, "source": os.path.basename(d.rstrip("/")),
+               "note": "FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md HBM section; separate --pmc passes"}
+        json.dump(out, open(traffic[1], "w"), indent=1)
+        print("wrote", traffic[1], out)
 
 
 if __name__ == "__main__":

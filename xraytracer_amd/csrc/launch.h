@@ -17,6 +17,7 @@ hipError_t launch_shade(const KParams& P, const uint32_t* list, const uint32_t* 
                         uint32_t* out_count, uint32_t* req_count, uint32_t blocks, hipStream_t st);
 // fused schedule (k_step): LDS bytes it needs for this scene, 0 = scene too large for it
 size_t step_lds_bytes(const KParams& P);
+bool use_step_tri(const KParams& P);   // triangle scene: k_step_tri (cooperative traces)
 // up to `visits` path segments per live slot; appends survivors to out (partitioned
 // counters out_count), low-RNG slots to P.req (req_count); clears zero (next-next round)
 // dP: device copy of P (the triangle-scene kernel reads its parameters from memory)

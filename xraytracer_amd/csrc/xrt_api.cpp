@@ -541,6 +541,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     HIPCHK(c, hipMemcpy(hs, P.stats, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     if (hs[5] || hs[6]) std::fprintf(stderr, "[xrt] triangle tests: lane %llu wave %llu\n", hs[5], hs[6]);
     S.segments = hs[0], S.shadow_rays = hs[1], S.draws = hs[2], S.rejected = hs[3], S.stalled = hs[4];
+    S.schedule = !fused ? XRT_SCHED_WAVEFRONT : use_step_tri(P) ? XRT_SCHED_STEP_TRI : XRT_SCHED_STEP;
     if (timing) {
         for (auto& u : ev_use) {
             float ms = 0.0f;
