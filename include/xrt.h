@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 3
+#define XRT_ABI_VERSION 4
 
 /* ---- status codes ---------------------------------------------------------------- */
 enum {
@@ -105,8 +105,10 @@ typedef struct {
 enum { XRT_INTEGRATOR_GI = 0, XRT_INTEGRATOR_DIRECT = 1, XRT_INTEGRATOR_VPT = 2 };
 enum {
     XRT_FLAG_TIMING = 1u,      /* time every kernel with HIP events (xrt_stats.kernel_ms)     */
-    XRT_FLAG_WAVEFRONT = 2u    /* force the multi-pass schedule (k_shade + k_trace) even when
+    XRT_FLAG_WAVEFRONT = 2u,   /* force the multi-pass schedule (k_shade + k_trace) even when
                                   the scene fits the fused LDS-resident schedule (k_step)     */
+    XRT_FLAG_NO_MERGED = 4u    /* triangle scenes: per-segment cooperative traces (k_step_tri)
+                                  instead of the merged shadow + extension traces             */
 };
 
 typedef struct {
@@ -125,8 +127,9 @@ enum {
 };
 
 /* device schedules: multi-pass wavefront (k_shade + k_trace), fused per-slot k_step with
- * the scene in LDS, and its triangle-scene form with cooperative (ray, triangle) traces */
-enum { XRT_SCHED_WAVEFRONT = 0, XRT_SCHED_STEP = 1, XRT_SCHED_STEP_TRI = 2 };
+ * the scene in LDS, its triangle-scene form with cooperative (ray, triangle) traces, and
+ * that form with one merged trace (shadow rays + next extension ray) per segment */
+enum { XRT_SCHED_WAVEFRONT = 0, XRT_SCHED_STEP = 1, XRT_SCHED_STEP_TRI = 2, XRT_SCHED_STEP_MERGED = 3 };
 
 typedef struct {
     double wall_ms;              /* host wall clock of the render call (upload excluded) */

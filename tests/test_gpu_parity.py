@@ -34,11 +34,17 @@ def renderer():
     r.close()
 
 
-@pytest.fixture(params=["auto", "wavefront"])
+@pytest.fixture(params=["auto", "step_tri", "wavefront"])
 def sched(request):
-    """Both device schedules: "auto" runs the fused LDS-resident k_step for scenes that fit
-    (every scene below except the C4 sphere mesh), "wavefront" forces k_shade + k_trace."""
+    """Every device schedule: "auto" runs the fused LDS-resident kernels for scenes that fit
+    (every scene below except the C4 sphere mesh) — small triangle scenes with merged
+    shadow + extension traces (k_step_merged); "step_tri" forces the per-ray-kind
+    cooperative traces (k_step_tri) for those; "wavefront" forces k_shade + k_trace."""
     return request.param
+
+
+EXPECT_TRI = {"auto": abi.XRT_SCHED_STEP_MERGED, "step_tri": abi.XRT_SCHED_STEP_TRI,
+              "wavefront": abi.XRT_SCHED_WAVEFRONT}
 
 
 def render_both(r, scene, w, h, spp, schedule="auto", **kw):
@@ -151,8 +157,8 @@ def test_c1_cornell_gi_bit_exact(renderer, sched):
     img, ref, st = render_both(renderer, s, 256, 256, 16, schedule=sched)
     compare(img, ref)
     g = renderer.stats
-    assert (g.launches[abi.XRT_K_STEP] > 0) == (sched == "auto")
-    assert g.schedule == (abi.XRT_SCHED_STEP_TRI if sched == "auto" else abi.XRT_SCHED_WAVEFRONT)
+    assert (g.launches[abi.XRT_K_STEP] > 0) == (sched != "wavefront")
+    assert g.schedule == EXPECT_TRI[sched]
     assert (g.segments, g.shadow_rays, g.draws, g.rejected) == (st["segments"], st["shadow_rays"], st["draws"],
                                                                 st["rejected"])
 
@@ -187,6 +193,35 @@ def test_spp_one_and_depth_zero(renderer, sched):
     assert np.all(img == 0) and np.all(ref == 0)
 
 
+@pytest.mark.parametrize("visits", [1, 2, 3, 7])
+def test_merged_segments_per_launch(renderer, visits, monkeypatch):
+    """The merged-trace kernel drains its shadow rays at every launch boundary and resumes
+    paths across launches: any number of segments per launch gives the same image and
+    counters (GI and Direct; one and two lights)."""
+    monkeypatch.setenv("XRT_STEP_VISITS", str(visits))
+    s = scenes.cornell(24, 18)
+    for kw in ({}, {"integrator": "direct"}, {"max_depth": 5}):
+        img, ref, st = render_both(renderer, s, 24, 18, 6, **kw)
+        compare(img, ref)
+        g = renderer.stats
+        assert g.schedule == abi.XRT_SCHED_STEP_MERGED
+        assert (g.segments, g.shadow_rays, g.draws) == (st["segments"], st["shadow_rays"], st["draws"])
+
+
+@pytest.mark.parametrize("spw", [16, 32, 64])
+def test_merged_slots_per_wave(renderer, spw, monkeypatch):
+    """Half- and quarter-filled waves (the merged kernel's layout for small pixel shards)
+    render the same image and counters as full waves."""
+    monkeypatch.setenv("XRT_MERGED_SPW", str(spw))
+    s = scenes.cornell(40, 30)
+    for kw in ({}, {"integrator": "direct"}):
+        img, ref, st = render_both(renderer, s, 40, 30, 5, **kw)
+        compare(img, ref)
+        g = renderer.stats
+        assert g.schedule == abi.XRT_SCHED_STEP_MERGED
+        assert (g.segments, g.shadow_rays, g.draws) == (st["segments"], st["shadow_rays"], st["draws"])
+
+
 def test_shards_reassemble_exactly(renderer):
     """Row-interleaved pixel shards (the multi-GPU split) sum to the 1-shard image bit-exactly."""
     s = scenes.cornell(48, 37)
@@ -207,7 +242,7 @@ def test_c3_spheres_direct(renderer, sched):
     s = scenes.spheres(160, 90)
     img, ref, st = render_both(renderer, s, 160, 90, 4, schedule=sched)
     compare(img, ref)
-    assert renderer.stats.schedule == (abi.XRT_SCHED_STEP if sched == "auto" else abi.XRT_SCHED_WAVEFRONT)
+    assert renderer.stats.schedule == (abi.XRT_SCHED_WAVEFRONT if sched == "wavefront" else abi.XRT_SCHED_STEP)
     assert renderer.stats.shadow_rays == st["shadow_rays"]
 
 

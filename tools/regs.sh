@@ -2,7 +2,7 @@
 # tools/regs.sh [pattern] — per-kernel VGPR/SGPR/spill/occupancy of wavefront.hip (gfx950)
 cd "$(dirname "$0")/../xraytracer_amd/csrc"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -ffp-contract=off -I../../include -I. --offload-arch=gfx950 \
-    -c wavefront.hip -o /tmp/regs_wf.o -Rpass-analysis=kernel-resource-usage 2>&1 |
+    $REGS_DEFS -c wavefront.hip -o /tmp/regs_wf.o -Rpass-analysis=kernel-resource-usage 2>&1 |
 python3 -c '
 import re, sys
 pat = sys.argv[1] if len(sys.argv) > 1 else ""

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #include "wavefront.h"
 
@@ -24,6 +26,17 @@ bool use_step_tri(const KParams& P);   // triangle scene: k_step_tri (cooperativ
 hipError_t launch_step(const KParams& P, const KParams* dP, const uint32_t* list, const uint32_t* count, uint32_t* out,
                        uint32_t* out_count, uint32_t* zero, uint32_t* req_count, uint32_t visits, uint32_t blocks,
                        hipStream_t st);
+// merged-trace triangle schedule (step_tri.hip): eligibility, RNG words one segment may
+// draw, LDS bytes, the per-object kernel-argument records, and the launch (same list /
+// counter contract as launch_step)
+bool use_step_merged(const KParams& P);
+uint32_t step_merged_draws(const KParams& P);
+uint32_t step_merged_spw(const KParams& P);   // path slots per wave of the merged kernel
+size_t step_merged_lds_bytes(const KParams& P);
+void build_step_objs(const DObjBox* boxes, int n, StepObjs& SO);
+hipError_t launch_step_merged(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
+                              const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
+                              uint32_t* req_count, uint32_t visits, uint32_t blocks, hipStream_t st);
 hipError_t launch_finish(const KParams& P, hipStream_t st);
 hipError_t launch_test_rng(const uint32_t* seeds, uint32_t n_seeds, uint32_t skip, uint32_t n, float* out,
                            uint32_t* rings, hipStream_t st);

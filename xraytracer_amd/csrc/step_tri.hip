@@ -1,0 +1,567 @@
+// step_tri.hip — merged-trace fused schedule for small triangle scenes (C1, C2: the
+// Cornell box), the latency-critical kernel of the renderer.
+//
+// Same per-pixel sequence as NormalRenderer::doRender + GIIntegrator / DirectIntegrator
+// (Src/renderer.cpp:29-81, Src/integrator.h:82-119, 205-287), one path slot per pixel, path
+// state in registers for `visits` segments per launch.  What differs from k_step_tri
+// (wavefront.hip) is the schedule of the traces:
+//
+//  * One cooperative trace per segment.  The NEE shadow rays of segment i and the
+//    extension ray of segment i+1 (or the next sample's camera ray) are traced together:
+//    every RNG draw of segment i (RR, light samples, BSDF sample, the next sample's jitter)
+//    happens in the reference's order before either ray is traced, and the occlusion
+//    result only changes the radiance, never a draw.  The contribution is kept for both
+//    outcomes (c1: visible, c0: occluded — the reference multiplies by vis first, so both
+//    are computed with its operation order) and added after the trace, still before any
+//    later radiance update of the same path, so every float sum happens in the
+//    reference's order.  A sample that ends with shadow rays in flight is finished after
+//    they resolve (rad_fin), while its successor's camera ray is traced.
+//  * Object-major pair passes: for each object (kernel-argument record, scalar loads) the
+//    wave ballots which of its rays (1 + NL per lane) overlap the object's culling box,
+//    ranks them (mbcnt, one LDS word each) and tests the (ray, triangle) pairs 64 per pass,
+//    pair j -> ray rank j / count (magic multiply), triangle first + j % count.  No prefix
+//    scan, no per-lane expansion loop.  Closest hits merge with an LDS atomicMin of
+//    (t bits << 32 | triangle): smallest t, ties to the lower triangle index — the
+//    reference's in-order strict `t < best` scan; shadow rays set an occlusion bit.
+//  * The RNG words a segment can use (6 + 2 NL at most) are prefetched into registers by
+//    global (not flat) loads issued one segment ahead.
+//
+// GIIntegrator with maxDepth 0 and scenes with more than kMergedMaxObjs objects keep using
+// k_step_tri.
+#include "launch.h"
+#include "path_common.h"
+
+namespace xrt {
+
+using gu32 = __attribute__((address_space(1))) const uint32_t;
+using gf32 = __attribute__((address_space(1))) const float;
+// global-address-space view of a generic pointer to device memory: global_load instead of
+// flat_load (a flat load also counts in lgkmcnt, so every LDS wait would wait for it too)
+template <class G, class T>
+__device__ __forceinline__ G* glb(T* p) {
+    return (G*)(p);
+}
+__device__ __forceinline__ v3 ld3g(const f4* p, size_t i) {
+    gf32* q = glb<gf32>(p) + 4 * i;
+    return mk(q[0], q[1], q[2]);
+}
+
+// Stream words of one slot held in registers: b[0] is the next draw.  A segment draws at
+// most NW words (checked before it starts), so there is no fallback load.
+template <int NW>
+struct RngRegs {
+    uint32_t b[NW];
+    uint32_t c;
+    __device__ __forceinline__ void load(const uint32_t* ring) {
+        gu32* r = glb<gu32>(ring);
+        uint32_t i = c % kRing;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+            b[j] = r[i];
+            i = (i + 1 == kRing) ? 0u : i + 1;
+        }
+    }
+    __device__ __forceinline__ float next() {
+        const uint32_t y = b[0];
+#pragma unroll
+        for (int j = 0; j + 1 < NW; ++j) b[j] = b[j + 1];
+        ++c;
+        return canonical(mt_temper(y));
+    }
+};
+
+template <int NL>
+struct MergedWave {
+    static constexpr int R = 1 + NL;   // rays per lane: extension + one shadow ray per light
+    f4 ro[R * 64];                     // origin, w = tmax (shadow rays)
+    f4 rd[R * 64];
+    unsigned long long best[64];       // closest hit of the extension ray: (t bits << 32) | tri
+    uint32_t occ[64];                  // bit l: shadow ray l is occluded
+    uint32_t list[R * 64];             // ranked rays (q * 64 + lane) of the current object
+};
+
+__device__ __forceinline__ uint32_t lanemask_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Conservative overlap of the ray segment [0, tlim] with the object's culling box.
+__device__ __forceinline__ bool obj_overlap(v3 o, v3 inv, const StepObj& B, float tlim) {
+    const float tx0 = (B.bmin[0] - o.x) * inv.x, tx1 = (B.bmax[0] - o.x) * inv.x;
+    const float ty0 = (B.bmin[1] - o.y) * inv.y, ty1 = (B.bmax[1] - o.y) * inv.y;
+    const float tz0 = (B.bmin[2] - o.z) * inv.z, tz1 = (B.bmax[2] - o.z) * inv.z;
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
+    return !(tn > tf);
+}
+
+// Mesh::rayTriangleIntersect (Src/primitive.cpp:140-168) without branches: the same float
+// operations, and the same accept/reject decisions (NaN comparisons included).
+__device__ __forceinline__ bool ray_tri_nb(v3 o, v3 d, v3 v0, v3 e1, v3 e2, float& t) {
+    const v3 pvec = cross(d, e2);
+    const float det = dot(e1, pvec);
+    const float invDet = 1.0f / det;
+    const v3 tvec = o - v0;
+    const float u = dot(tvec, pvec) * invDet;
+    const v3 qvec = cross(tvec, e1);
+    const float v = dot(d, qvec) * invDet;
+    t = dot(e2, qvec) * invDet;
+    const bool rej = (__builtin_fabsf(det) < kEPSILON) | (u < 0.0f) | (u > 1.0f) | (v < 0.0f) | (u + v > 1.0f);
+    return !rej & (t > kEPSILON);
+}
+
+// One cooperative trace of the wave: the extension ray (closest hit, if `ext`) and the
+// pending shadow rays (any hit, bits of `shm`; already stored in W by the shading code).
+template <int NL>
+__device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L, MergedWave<NL>& W, int lane,
+                                             bool ext, v3 o, v3 d, uint32_t shm, const v3 (&so)[NL + 1],
+                                             const v3 (&sd)[NL + 1], const float (&stm)[NL + 1],
+                                             unsigned long long& best, uint32_t& occ) {
+    constexpr int R = 1 + NL;
+    W.best[lane] = ~0ull;
+    W.occ[lane] = 0u;
+    W.ro[lane] = make_float4(o.x, o.y, o.z, kINF);
+    W.rd[lane] = make_float4(d.x, d.y, d.z, 0.0f);
+    v3 inv[R];
+    inv[0] = rcp3(d);
+#pragma unroll
+    for (int l = 0; l < NL; ++l) inv[1 + l] = rcp3(sd[l]);
+    wave_sync();
+    const int n = SO.n;
+    for (int ob = 0; ob < n; ++ob) {
+        const StepObj& B = SO.o[ob];
+        bool need[R];
+        need[0] = ext && obj_overlap(o, inv[0], B, kINF);
+#pragma unroll
+        for (int l = 0; l < NL; ++l)
+            need[1 + l] = B.occluder && ((shm >> l) & 1u) && obj_overlap(so[l], inv[1 + l], B, stm[l]);
+        uint32_t tot = 0;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const uint64_t m = __ballot(need[q]);
+            if (need[q]) W.list[tot + lanemask_rank(m)] = (uint32_t)(q * 64 + lane);
+            tot += (uint32_t)__popcll(m);
+        }
+        if (tot == 0) continue;
+        wave_sync();
+        const uint32_t c = B.count, first = (uint32_t)B.first, magic = B.magic;
+        const uint32_t pairs = tot * c;
+        for (uint32_t j0 = 0; j0 < pairs; j0 += 64) {
+            const uint32_t j = j0 + (uint32_t)lane;
+            if (j < pairs) {
+                const uint32_t r = (c == 1u) ? j : __umulhi(j, magic);
+                const uint32_t k = first + (j - r * c);
+                const uint32_t e = W.list[r];
+                const f4 A = W.ro[e];
+                const f4 D = W.rd[e];
+                float t;
+                const bool hit = ray_tri_nb(xyz(A), xyz(D), xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]),
+                                            xyz(L.tri[3 * k + 2]), t);
+                if (hit) {
+                    if (e < 64u)
+                        atomicMin(&W.best[e], ((unsigned long long)__float_as_uint(t) << 32) | k);
+                    else if (t < A.w)
+                        atomicOr(&W.occ[e & 63u], 1u << ((e >> 6) - 1u));
+                }
+            }
+        }
+        wave_sync();
+    }
+    best = W.best[lane];
+    occ = W.occ[lane];
+}
+
+#ifdef XRT_PHASE_CLOCK
+#define MPH_DECL uint64_t ph_t = __builtin_amdgcn_s_memtime();
+#define MPH_MARK(i)                                          \
+    do {                                                     \
+        const uint64_t ph_n = __builtin_amdgcn_s_memtime();  \
+        ph_acc[i] += ph_n - ph_t;                            \
+        ph_t = ph_n;                                         \
+    } while (0)
+#else
+#define MPH_DECL
+#define MPH_MARK(i) \
+    do {            \
+    } while (0)
+#endif
+
+#ifndef XRT_STEP_WAVES
+#define XRT_STEP_WAVES 4
+#endif
+
+// SPW: path slots per wave (64, 32 or 16).  Lanes >= SPW own no slot but take part in
+// every pair pass of the cooperative traces, so a half- or quarter-filled wave traces its
+// rays in proportionally fewer passes; with few slots per GPU (a pixel shard of a
+// multi-GPU frame) this puts more, shorter waves on every SIMD.
+template <int INTEG, int NL, int SPW>
+__global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
+    const KParams* __restrict__ Pp, const StepObjs SO, const uint32_t* __restrict__ list,
+    const uint32_t* __restrict__ count, uint32_t* __restrict__ out, uint32_t* out_count, uint32_t* zero_count,
+    uint32_t* req_count, uint32_t visits) {
+    constexpr int NW = 6 + 2 * NL;   // most words one segment draws (see the header)
+    const KParams& P = *Pp;
+    extern __shared__ __attribute__((aligned(16))) f4 lds_m[];
+    char* lb = reinterpret_cast<char*>(lds_m);
+    const StepLayout Lo = step_layout(P);
+    LScene L;
+    L.tri = reinterpret_cast<const f4*>(lb + Lo.tri);
+    L.tng = reinterpret_cast<const f4*>(lb + Lo.tng);
+    L.nrm = reinterpret_cast<const f4*>(lb + Lo.nrm);
+    L.box = reinterpret_cast<const DObjBox*>(lb + Lo.box);
+    L.sph = reinterpret_cast<const f4*>(lb + Lo.sph);
+    L.bx = reinterpret_cast<const f4*>(lb + Lo.bx);
+    L.obj = reinterpret_cast<const DObj*>(lb + Lo.obj);
+    L.light = reinterpret_cast<const DLight*>(lb + Lo.light);
+    L.sobj = reinterpret_cast<const int*>(lb + Lo.sobj);
+    const int tid = threadIdx.x, lane = tid & 63;
+    MergedWave<NL>& W = reinterpret_cast<MergedWave<NL>*>(lb + ((Lo.total + 15u) & ~15u))[tid >> 6];
+    lds_copy(const_cast<f4*>(L.tri), P.tri, 3 * P.n_tris, tid);
+    lds_copy(const_cast<f4*>(L.tng), P.tri_ng, P.n_tris, tid);
+    lds_copy(const_cast<f4*>(L.nrm), P.tri_nrm, 3 * P.n_tris, tid);
+    lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
+    lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid);
+    __syncthreads();
+#ifdef XRT_PHASE_CLOCK
+    uint64_t ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t ph_vis = 0;
+    const uint64_t kt0 = __builtin_amdgcn_s_memtime();
+#endif
+    zero_parts(P, zero_count);
+    const PartIter it = part_iter(P, count, (kBlock / 64) * SPW);
+    const uint32_t spp = P.spp, max_depth = P.max_depth, width = P.width, height = P.height;
+    for (uint32_t base = it.first; base < it.n; base += it.stride) {
+        const uint32_t i = base + (uint32_t)(tid >> 6) * SPW + (uint32_t)lane;
+        const bool own = lane < SPW && i < it.n;
+        const uint32_t s = own ? list[it.p * P.part_cap + i] : 0;
+        uint32_t st = own ? glb<gu32>(P.state)[s] : ST_DONE;
+        const bool live = !(st & ST_DONE);
+        uint32_t g = 0, depth = 0, k = 0, kst = 0;   // k: finished samples, kst: started samples
+        RngRegs<NW> rng;
+        rng.c = 0;
+        const uint32_t* ring = P.ring + (size_t)s * kRing;
+        v3 thr = mk(1, 1, 1), rad = mk(0, 0, 0), o = mk(0, 0, 0), d = mk(0, 0, 0), acc = mk(0, 0, 0);
+        v3 rad_fin = mk(0, 0, 0), thr_nee = mk(0, 0, 0);
+        v3 so[NL + 1], sd[NL + 1], c1[NL + 1], c0[NL + 1];
+        float stm[NL + 1];
+#pragma unroll
+        for (int l = 0; l <= NL; ++l) so[l] = sd[l] = c1[l] = c0[l] = mk(0, 0, 0), stm[l] = 0.0f;
+        uint32_t shm = 0;          // shadow rays in flight (bit per light)
+        bool ext = false, fin = false;
+        const uint32_t col = s % width, row = P.shard_index + P.shard_count * (s / width);
+        float* px = P.fb + 3 * ((size_t)col + (size_t)width * row);
+        if (live) {
+            g = glb<gu32>(P.rng_g)[s];
+            rng.c = glb<gu32>(P.rng_c)[s];
+            depth = glb<gu32>(P.depth)[s];
+            k = glb<gu32>(P.sample_k)[s];
+            kst = k;
+            if (!(st & ST_REGEN)) {
+                thr = ld3g(P.thr, s), rad = ld3g(P.rad, s);
+                o = ld3g(P.ray_o, s), d = ld3g(P.ray_d, s);
+                ext = true;
+                kst = k + 1;
+            }
+            gf32* pxg = glb<gf32>(px);
+            acc = mk(pxg[0], pxg[1], pxg[2]);
+            rng.load(ring);
+        }
+        uint32_t nseg = 0, nsh = 0, nrej = 0;
+        // Image::addPixel of a finished sample (Src/renderer.cpp:57-75)
+        auto finish = [&](v3 r0) {
+            const v3 r = r0 / 1.0f;
+            if (__builtin_isnan(r.x) || __builtin_isnan(r.y) || __builtin_isnan(r.z) || __builtin_isinf(r.x) ||
+                __builtin_isinf(r.y) || __builtin_isinf(r.z) || r.x < 0.0f || r.y < 0.0f || r.z < 0.0f) {
+                ++nrej;
+            } else {
+                acc = acc + r;
+            }
+            ++k;
+            if (k >= spp) st = ST_DONE;
+        };
+        // jitter draws + PinholeCamera::sampleRay for the next sample (Src/renderer.cpp:44-50)
+        auto start_sample = [&]() {
+            const float u = ((float)(int)col + rng.next()) / (float)width;
+            const float v = ((float)(int)row + rng.next()) / (float)height;
+            camera_ray(P, u, v, o, d);
+            thr = mk(1, 1, 1), rad = mk(0, 0, 0);
+            depth = 0;
+            ext = true;
+            ++kst;
+        };
+        // add the resolved NEE of the last shaded segment (GI: rad += thr * directL;
+        // Direct: L += L_light per light) and finish its sample if it ended there
+        auto resolve = [&](uint32_t occ) {
+            if (!shm) return;
+            v3& tgt = fin ? rad_fin : rad;
+            if (INTEG == XRT_INTEGRATOR_DIRECT) {
+#pragma unroll
+                for (int l = 0; l < NL; ++l)
+                    if ((shm >> l) & 1u) tgt = tgt + (((occ >> l) & 1u) ? c0[l] : c1[l]);
+            } else {
+                v3 directL = mk(0, 0, 0);
+#pragma unroll
+                for (int l = 0; l < NL; ++l)
+                    if ((shm >> l) & 1u) {
+                        const v3 L_light = mk(0, 0, 0) + (((occ >> l) & 1u) ? c0[l] : c1[l]);
+                        directL = directL + L_light;
+                    }
+                tgt = tgt + thr_nee * directL;
+            }
+            shm = 0;
+            if (fin) {
+                fin = false;
+                finish(rad_fin);
+            }
+        };
+        MPH_DECL
+        for (uint32_t vis = 0; vis < visits; ++vis) {
+            const bool act = live && !(st & ST_DONE) && g - rng.c >= (uint32_t)NW;
+            if (!__ballot(act || shm)) break;
+            if (act && (st & ST_REGEN)) {
+                st &= ~ST_REGEN;
+                start_sample();
+            }
+            const bool ext_now = act && ext;
+            MPH_MARK(0);
+            unsigned long long best;
+            uint32_t occ;
+            merged_trace<NL>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
+            MPH_MARK(1);
+            resolve(occ);
+            MPH_MARK(2);
+            if (ext_now) {
+                ++nseg;
+                int hk = -1, obj = -1;
+                float ht = kINF, hu = 0.0f, hv = 0.0f;
+                if (best != ~0ull) {
+                    hk = (int)(uint32_t)best;
+                    (void)ray_tri(o, d, xyz(L.tri[3 * hk]), xyz(L.tri[3 * hk + 1]), xyz(L.tri[3 * hk + 2]), ht, hu,
+                                  hv);
+                    obj = __float_as_int(L.tri[3 * hk].w);
+                }
+                v3 pos = mk(0, 0, 0), ng = mk(0, 0, 0);
+                if (hk >= 0) pos = ray_at(o, d, ht), ng = xyz(L.tng[hk]);
+                bool ended = false, alive = false;
+                if (INTEG == XRT_INTEGRATOR_DIRECT) {
+                    // DirectIntegrator::integrate (Src/integrator.h:82-119)
+                    if (obj < 0) {
+                        rad = mk((float)0.18, (float)0.18, (float)0.18);
+                        ended = true;
+                    } else if (L.obj[obj].light >= 0) {
+                        rad = light_Le(L.light[L.obj[obj].light], tri_ns_l(L, hk, hu, hv), d);
+                        ended = true;
+                    } else {
+                        alive = true;
+                    }
+                } else {
+                    // GIIntegrator::integrate loop body (Src/integrator.h:214-284)
+                    if (obj < 0) {
+                        rad = rad + thr * mk(0.0f, 0.0f, 0.0f);
+                        ended = true;
+                    } else {
+                        alive = true;
+                        if (depth > 0) {
+                            const float pr = smin((thr.x + thr.y + thr.z) / 3.0f, 1.0f);
+                            if (rng.next() >= pr) alive = false, ended = true;
+                            else thr = thr / mk(pr, pr, pr);
+                        }
+                        if (alive && L.obj[obj].light >= 0) {
+                            if (depth == 0)
+                                rad = rad + thr * light_Le(L.light[L.obj[obj].light], tri_ns_l(L, hk, hu, hv), d);
+                            alive = false, ended = true;
+                        }
+                    }
+                }
+                if (alive) {
+                    // next-event estimation: light samples now, shadow rays traced with the
+                    // next trace of the wave
+                    const DObj& ob = L.obj[obj];
+                    const v3 fr = ob.material == 1 ? mk(ob.fr[0], ob.fr[1], ob.fr[2]) : mk(0, 0, 0);
+#pragma unroll
+                    for (int l = 0; l < NL; ++l) {
+                        v3 wi = mk(0, 0, 0);
+                        float tmax = 0.0f, pdf = 0.0f;
+                        const v3 Lv = light_sample(L.light[l], pos, wi, pdf, tmax, rng);
+                        if (pdf != 0.0f) {
+                            ++nsh;
+                            shm |= 1u << l;
+                            const float bias = 0.01f;
+                            so[l] = pos + ng * bias, sd[l] = wi, stm[l] = tmax - bias;
+                            W.ro[(1 + l) * 64 + lane] = make_float4(so[l].x, so[l].y, so[l].z, stm[l]);
+                            W.rd[(1 + l) * 64 + lane] = make_float4(wi.x, wi.y, wi.z, 0.0f);
+                            const float cosv = smax(0.0f, dot(ng, wi));
+                            // vis * fr * L * cos / pdf (Src/integrator.h:250-262) for vis = 1, 0
+                            c1[l] = (((fr * 1.0f) * Lv) * cosv) / pdf;
+                            c0[l] = (((fr * 0.0f) * Lv) * cosv) / pdf;
+                        }
+                    }
+                    if (INTEG == XRT_INTEGRATOR_DIRECT) {
+                        ended = true;
+                    } else {
+                        if (shm) thr_nee = thr;
+                        else rad = rad + thr * mk(0.0f, 0.0f, 0.0f);   // no shadow ray: directL = 0
+                        float pdf = 1.0f;
+                        v3 nd = mk(0, 0, 0);
+                        if (ob.material == 1) {
+                            v3 dpdu, dpdv;
+                            onb(tri_ns_l(L, hk, hu, hv), dpdu, dpdv);
+                            nd = lambert_sample_f(ng, dpdu, dpdv, rng);
+                            pdf = 1.0f / (2.0f * kPI);
+                        }
+                        const float cosv = smax(0.0f, dot(nd, ng));
+                        thr = thr * ((fr * cosv) / pdf);
+                        o = pos + ng * 0.01f;
+                        d = nd;
+                        ++depth;
+                        if (depth >= max_depth) ended = true;
+                    }
+                }
+                if (ended) {
+                    ext = false;
+                    if (shm) {
+                        rad_fin = rad;
+                        fin = true;
+                    } else {
+                        finish(rad);
+                    }
+                    if (kst < spp) start_sample();
+                }
+            }
+            MPH_MARK(3);
+            if (act) rng.load(ring);
+#ifdef XRT_PHASE_CLOCK
+            ++ph_vis;
+#endif
+            MPH_MARK(4);
+        }
+        // drain: trace the shadow rays still in flight, so no NEE state crosses launches
+        if (__ballot(shm != 0)) {
+            unsigned long long best;
+            uint32_t occ;
+            merged_trace<NL>(SO, L, W, lane, false, o, d, shm, so, sd, stm, best, occ);
+            resolve(occ);
+        }
+        MPH_MARK(5);
+        bool want_req = false;
+        if (live) {
+            px[0] = acc.x, px[1] = acc.y, px[2] = acc.z;
+            want_req = !(st & (ST_DONE | ST_RNGREQ)) && g - rng.c < P.rng_keep;
+            if (want_req) st |= ST_RNGREQ;
+            P.state[s] = st;
+            if (!(st & (ST_DONE | ST_REGEN))) {
+                P.depth[s] = depth;
+                P.thr[s] = pk(thr);
+                P.rad[s] = pk(rad);
+                P.ray_o[s] = pk(o);
+                P.ray_d[s] = pk(d);
+            }
+            P.sample_k[s] = k;
+            P.rng_c[s] = rng.c;
+            if (nseg) P.c_seg[s] += nseg;
+            if (nsh) P.c_shadow[s] += nsh;
+            if (nrej) P.c_rej[s] += nrej;
+        }
+        wave_append(live && !(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
+        wave_append(want_req, s, P.req + it.p * P.part_cap, req_count + it.p, lane);
+    }
+#ifdef XRT_PHASE_CLOCK
+    if (lane == 0) {
+        for (int q = 0; q < 8; ++q) atomicAdd(P.stats + 8 + q, (unsigned long long)ph_acc[q]);
+        atomicAdd(P.stats + 16, (unsigned long long)(__builtin_amdgcn_s_memtime() - kt0));
+        atomicAdd(P.stats + 20, (unsigned long long)ph_vis);
+    }
+#endif
+}
+
+// ------------------------------------------------------------------- host side ----
+bool use_step_merged(const KParams& P) {
+    return P.scene_kind == SCN_TRI && P.small_tri && P.n_objs <= kMergedMaxObjs && P.n_lights <= kMaxLights &&
+           (P.integrator == XRT_INTEGRATOR_DIRECT || (P.integrator == XRT_INTEGRATOR_GI && P.max_depth > 0)) &&
+           !std::getenv("XRT_NO_MERGED") && step_merged_lds_bytes(P) <= kStepLds;
+}
+
+uint32_t step_merged_draws(const KParams& P) { return 6u + 2u * (uint32_t)P.n_lights; }
+
+size_t step_merged_lds_bytes(const KParams& P) {
+    size_t w = 0;
+    switch (P.n_lights) {
+        case 0: w = sizeof(MergedWave<0>); break;
+        case 1: w = sizeof(MergedWave<1>); break;
+        case 2: w = sizeof(MergedWave<2>); break;
+        case 3: w = sizeof(MergedWave<3>); break;
+        default: w = sizeof(MergedWave<4>); break;
+    }
+    return ((step_layout(P).total + 15u) & ~15u) + (kBlock / 64) * w;
+}
+
+void build_step_objs(const DObjBox* boxes, int n, StepObjs& SO) {
+    std::memset(&SO, 0, sizeof(SO));
+    SO.n = n;
+    for (int i = 0; i < n; ++i) {
+        StepObj& o = SO.o[i];
+        for (int q = 0; q < 3; ++q) o.bmin[q] = boxes[i].bmin[q], o.bmax[q] = boxes[i].bmax[q];
+        o.first = boxes[i].first;
+        o.count = (uint32_t)(boxes[i].count_occ & 0x7fffffff);
+        o.occluder = boxes[i].count_occ < 0 ? 1u : 0u;
+        // ceil(2^32 / count): floor(j * magic / 2^32) = j / count for j * count < 2^32
+        o.magic = o.count > 1 ? (uint32_t)(((1ull << 32) + o.count - 1) / o.count) : 0u;
+    }
+}
+
+template <int INTEG, int SPW>
+static void launch_merged_i(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
+                            const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
+                            uint32_t* req_count, uint32_t visits, size_t lds, hipStream_t st) {
+    const uint32_t per_block = (kBlock / 64) * SPW;
+    const uint32_t blocks = P.n_part * ((P.part_cap + per_block - 1) / per_block);
+#define XRT_LAUNCH_MERGED(NLV)                                                                                       \
+    hipLaunchKernelGGL((k_step_merged<INTEG, NLV, SPW>), dim3(blocks), dim3(kBlock), lds, st, dP, SO, list, count, \
+                       out, out_count, zero, req_count, visits)
+    switch (P.n_lights) {
+        case 0: XRT_LAUNCH_MERGED(0); break;
+        case 1: XRT_LAUNCH_MERGED(1); break;
+        case 2: XRT_LAUNCH_MERGED(2); break;
+        case 3: XRT_LAUNCH_MERGED(3); break;
+        default: XRT_LAUNCH_MERGED(4); break;
+    }
+#undef XRT_LAUNCH_MERGED
+}
+
+// slots per wave: as many as keep >= kMergedWavesWanted waves in flight for this shard
+// (XRT_MERGED_SPW overrides, for experiments; results do not depend on it)
+uint32_t step_merged_spw(const KParams& P) {
+    if (const char* e = std::getenv("XRT_MERGED_SPW")) {
+        const int v = std::atoi(e);
+        if (v == 16 || v == 32 || v == 64) return (uint32_t)v;
+    }
+    if (P.n_slots >= 64u * kMergedWavesWanted) return 64;
+    if (P.n_slots >= 32u * kMergedWavesWanted) return 32;
+    return 16;
+}
+
+template <int INTEG>
+static void launch_merged_spw(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
+                              const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
+                              uint32_t* req_count, uint32_t visits, size_t lds, hipStream_t st) {
+    switch (step_merged_spw(P)) {
+        case 64: launch_merged_i<INTEG, 64>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, lds, st); break;
+        case 32: launch_merged_i<INTEG, 32>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, lds, st); break;
+        default: launch_merged_i<INTEG, 16>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, lds, st); break;
+    }
+}
+
+hipError_t launch_step_merged(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
+                              const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
+                              uint32_t* req_count, uint32_t visits, uint32_t blocks, hipStream_t st) {
+    (void)blocks;   // the grid follows the slots-per-wave choice
+    const size_t lds = step_merged_lds_bytes(P);
+    if (P.integrator == XRT_INTEGRATOR_DIRECT)
+        launch_merged_spw<XRT_INTEGRATOR_DIRECT>(P, dP, SO, list, count, out, out_count, zero, req_count, visits,
+                                                 lds, st);
+    else
+        launch_merged_spw<XRT_INTEGRATOR_GI>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, lds,
+                                             st);
+    return hipGetLastError();
+}
+
+}  // namespace xrt

@@ -30,6 +30,8 @@ constexpr uint32_t kRngVisit = 16;   // a slot visit needs at least this many (m
 constexpr uint32_t kMaxParts = 64;   // live-list partitions (counters per list)
 constexpr uint32_t kRefillEvery = 4; // wavefront schedule: k_refill after every 4th k_shade
 constexpr uint32_t kStepVisits = 32; // fused schedule: path segments per slot per k_step
+constexpr uint32_t kMergedVisits = 32; // merged-trace schedule: segments per slot per launch
+constexpr uint32_t kMergedWavesWanted = 4096; // merged-trace schedule: waves to keep in flight (4 per SIMD)
 constexpr uint32_t kStepRefill = 1;  // fused schedule: k_refill after every k_step
 constexpr uint32_t kVisitDraws = 13; // max RNG draws of one GI/Direct segment (4 lights)
 // fused schedule: a slot queues a refill when fewer than refill * visits * 13 + kRngVisit
@@ -56,8 +58,8 @@ struct DSeg {   // a run of consecutive objects of one kind, in iteration order
 
 struct DObj {
     int kind, material, light, medium;
-    float albedo[3];
-    float pad;
+    float fr[3];   // Lambert::evaluateBxDF = albedo / PI (material 1), computed once on the host
+    float pad;     // with the same correctly rounded float division; 0 for other materials
 };
 
 // Mesh object culling record for small triangle scenes: the object's triangle range and
@@ -69,6 +71,23 @@ struct DObjBox {
     int first;
     float bmax[3];
     int count_occ;   // triangle count | (occluder << 31)
+};
+// Per-object record of the merged-trace triangle kernel (step_tri.hip), passed by value
+// as a kernel argument so the object loop reads it with scalar loads: the culling box
+// (DObjBox's, margin included), the triangle range, whether it occludes (no area light),
+// and magic = ceil(2^32 / count) for the pair -> (ray rank, triangle) split.
+struct StepObj {
+    float bmin[3];
+    int first;
+    float bmax[3];
+    uint32_t count;
+    uint32_t magic;
+    uint32_t occluder;
+};
+constexpr int kMergedMaxObjs = 32;
+struct StepObjs {
+    StepObj o[kMergedMaxObjs];
+    int n;
 };
 constexpr int kSmallTris = 1024;   // scenes up to this size keep every triangle in LDS
 constexpr int kSmallObjs = 256;

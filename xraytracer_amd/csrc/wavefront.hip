@@ -15,149 +15,9 @@
 // (Src/renderer.cpp:29-81).
 #include <hip/hip_runtime.h>
 
-#include "device_math.h"
-#include "wavefront.h"
-#include "xrt.h"
+#include "path_common.h"
 
 namespace xrt {
-
-constexpr int kBlock = 256;
-constexpr int kTriTile = 512;    // triangles per LDS tile (24 KiB)
-constexpr int kSphTile = 1024;   // spheres per LDS tile (16 KiB + 4 KiB)
-
-// ============================================================================ RNG ====
-__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
-    y ^= (y >> 11);
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
-    y ^= (y >> 18);
-    return y;
-}
-// generate_canonical<float,24>: (float)x / 2^32, nextafter(1,0) if it rounds to 1
-__device__ __forceinline__ float canonical(uint32_t y) {
-    const float f = (float)y * 0x1p-32f;
-    return f >= 1.0f ? 0x1.fffffep-1f : f;
-}
-__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
-    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
-    return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-}
-
-// A slot's stream: ring words x[c], x[c+1], ...  prefetch() issues the loads of the next 8
-// words at once (one memory latency for a whole shade pass instead of one per draw);
-// draws beyond the prefetched words are loaded on demand.
-struct Rng {
-    const uint32_t* ring;
-    uint32_t c;
-    uint32_t nb = 0;
-    uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0, b4 = 0, b5 = 0, b6 = 0, b7 = 0;
-    __device__ __forceinline__ void prefetch(uint32_t avail) {
-        nb = avail < 8u ? avail : 8u;
-        b0 = ring[c % kRing], b1 = ring[(c + 1) % kRing], b2 = ring[(c + 2) % kRing], b3 = ring[(c + 3) % kRing];
-        b4 = ring[(c + 4) % kRing], b5 = ring[(c + 5) % kRing], b6 = ring[(c + 6) % kRing], b7 = ring[(c + 7) % kRing];
-    }
-    __device__ __forceinline__ float next() {
-        uint32_t y;
-        if (nb) {
-            y = b0;
-            b0 = b1, b1 = b2, b2 = b3, b3 = b4, b4 = b5, b5 = b6, b6 = b7;
-            --nb;
-        } else {
-            y = ring[c % kRing];
-        }
-        ++c;
-        return canonical(mt_temper(y));
-    }
-};
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// One mt19937 twist of a slot's stream done by a whole wave: x[g+k] = x[g+k-227] ^
-// mix(x[g+k-624], x[g+k-623]) for k = 0..623 (libstdc++ _M_gen_rand).  Split into the
-// chunks k = m, 227 + m, 454 + m (m = lane + 64 j), the word each chunk needs from the
-// previous one, x[g+k-227], is the same lane's register — no LDS, no barrier.  The new
-// block lands in ring half g % 1248, over the oldest (fully consumed) block.  Must be
-// called by every lane of the wave.
-__device__ void wave_twist(uint32_t* ring, uint32_t g, int lane) {
-    const uint32_t h = g % kRing;
-    const uint32_t* old = ring + (kMT - h);
-    uint32_t* nw = ring + h;
-    uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t m = lane + 64 * j;
-        if (m < 227) a[j] = old[m + 397] ^ mt_mix(old[m], old[m + 1]);
-    }
-    const uint32_t n0 = __shfl(a[0], 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t m = lane + 64 * j;
-        if (m < 227) b[j] = a[j] ^ mt_mix(old[227 + m], old[228 + m]);
-    }
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const uint32_t m = lane + 64 * j;
-        if (m < 170) nw[454 + m] = b[j] ^ mt_mix(old[454 + m], m + 455 < kMT ? old[455 + m] : n0);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t m = lane + 64 * j;
-        if (m < 227) nw[m] = a[j], nw[227 + m] = b[j];
-    }
-}
-
-// In-kernel refill for the RNG self-test: every lane with `need` gets its next block.
-// Must be called by every lane of the wave (wave-uniform control flow).
-__device__ void wave_refill(bool need, uint32_t slot, uint32_t& g, uint32_t* rings, int lane) {
-    uint64_t m = __ballot(need);
-    if (m == 0) return;
-    while (m) {
-        const int L = __ffsll((unsigned long long)m) - 1;
-        m &= m - 1;
-        const uint32_t sl = __shfl(slot, L);
-        const uint32_t gl = __shfl(g, L);
-        wave_twist(rings + (size_t)sl * kRing, gl, lane);
-    }
-    if (need) g += kMT;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-}
-
-// Append v to list (count at cnt) for every lane with want set: one atomic per wave.
-// Must be called by every lane of the wave (wave-uniform control flow).
-__device__ __forceinline__ void wave_append(bool want, uint32_t v, uint32_t* list, uint32_t* cnt, int lane) {
-    const uint64_t m = __ballot(want);
-    if (!m) return;
-    const int leader = __ffsll((unsigned long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(cnt, (uint32_t)__popcll(m));
-    base = __shfl(base, leader);
-    if (want) list[base + __popcll(m & ((1ull << lane) - 1ull))] = v;
-}
-
-// Live and refill lists are partitioned: partition p owns the slots
-// [p*part_cap, (p+1)*part_cap) and its entries list[p*part_cap + i], i < count[p]; block b
-// serves partition b % n_part (grids are n_part * chunks blocks).  Appends then contend
-// on n_part counters instead of one, and a partition's slots are always touched by the
-// same XCD (blocks are dealt to the 8 XCDs round-robin and n_part is a multiple of 8).
-struct PartIter {
-    uint32_t p, first, stride, n;
-};
-__device__ __forceinline__ PartIter part_iter(const KParams& P, const uint32_t* count, uint32_t per_block) {
-    PartIter it;
-    it.p = blockIdx.x % P.n_part;
-    const uint32_t chunk = blockIdx.x / P.n_part, nchunks = gridDim.x / P.n_part;
-    it.first = chunk * per_block;
-    it.stride = nchunks * per_block;
-    it.n = count[it.p];
-    return it;
-}
-__device__ __forceinline__ void zero_parts(const KParams& P, uint32_t* c) {
-    if (blockIdx.x == 0 && threadIdx.x < P.n_part) c[threadIdx.x] = 0;
-}
 
 // k_refill: one wave per requested slot twists the next 624 words of its stream into the
 // consumed half of its ring (wave_twist), all requests in parallel across the chip.
@@ -176,63 +36,6 @@ __global__ __launch_bounds__(kBlock) void k_refill(KParams P, const uint32_t* __
             P.state[s] &= ~ST_RNGREQ;
         }
     }
-}
-
-// ====================================================================== geometry ====
-// Mesh::rayTriangleIntersect, no CULLING (Src/primitive.cpp:140-168), with e1 = v1 - v0,
-// e2 = v2 - v0 precomputed on the host by the same subtraction.
-__device__ __forceinline__ bool ray_tri(v3 o, v3 d, v3 v0, v3 e1, v3 e2, float& t, float& u, float& v) {
-    const v3 pvec = cross(d, e2);
-    const float det = dot(e1, pvec);
-    if (__builtin_fabsf(det) < kEPSILON) return false;
-    const float invDet = 1.0f / det;
-    const v3 tvec = o - v0;
-    u = dot(tvec, pvec) * invDet;
-    if (u < 0.0f || u > 1.0f) return false;
-    const v3 qvec = cross(tvec, e1);
-    v = dot(d, qvec) * invDet;
-    if (v < 0.0f || u + v > 1.0f) return false;
-    t = dot(e2, qvec) * invDet;
-    return t > kEPSILON;
-}
-
-// Sphere::doIntersect + solveQuadratic (Src/primitive.h:133-177): double -0.5*(b±sqrt)
-__device__ __forceinline__ bool sphere_hit(v3 o, v3 d, v3 c, float r, float& tnear) {
-    const v3 L = o - c;
-    const float a = dot(d, d);
-    const float b = 2.0f * dot(d, L);
-    const float cc = dot(L, L) - r * r;
-    const float discr = b * b - 4.0f * a * cc;
-    if (discr < 0.0f) return false;
-    float t0, t1;
-    if (discr == 0.0f) {
-        t0 = t1 = (float)(-0.5 * (double)b / (double)a);
-    } else {
-        const double sq = __builtin_sqrt((double)discr);
-        const float q = (b > 0.0f) ? (float)(-0.5 * ((double)b + sq)) : (float)(-0.5 * ((double)b - sq));
-        t0 = q / a;
-        t1 = cc / q;
-    }
-    if (t0 > t1) { const float tmp = t0; t0 = t1; t1 = tmp; }
-    if (t0 < 0.0f) {
-        t0 = t1;
-        if (t0 < 0.0f) return false;
-    }
-    tnear = t0;
-    return true;
-}
-
-// BoxMesh::intersect slab test (Src/primitive.h:243-264)
-__device__ __forceinline__ bool box_hit(v3 o, v3 d, v3 pmin, v3 pmax, float& t0, float& t1) {
-    const v3 di = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const v3 tt = di * (pmax - o), tb = di * (pmin - o);
-    const v3 tmin = mk(smin(tt.x, tb.x), smin(tt.y, tb.y), smin(tt.z, tb.z));
-    const v3 tmax = mk(smax(tt.x, tb.x), smax(tt.y, tb.y), smax(tt.z, tb.z));
-    t0 = smax(smax(tmin.x, tmin.y), tmin.z);
-    t1 = smin(smin(tmax.x, tmax.y), tmax.z);
-    if (t0 > t1 || t1 <= 0.0f) return false;
-    t0 = smax(t0, 0.0f);
-    return true;
 }
 
 // ==================================================================== k_seed ====
@@ -415,21 +218,6 @@ __global__ __launch_bounds__(kBlock) void k_trace(KParams P, const uint32_t* __r
     }
 }
 
-// Conservative ray/AABB overlap on [0, tlim] for culling (approximate reciprocal is fine:
-// the boxes carry a margin; fminf/fmaxf drop the NaNs of 0*inf, which only widens the
-// interval).
-__device__ __forceinline__ bool box_overlap(v3 o, v3 inv, const DObjBox& B, float tlim) {
-    const float tx0 = (B.bmin[0] - o.x) * inv.x, tx1 = (B.bmax[0] - o.x) * inv.x;
-    const float ty0 = (B.bmin[1] - o.y) * inv.y, ty1 = (B.bmax[1] - o.y) * inv.y;
-    const float tz0 = (B.bmin[2] - o.z) * inv.z, tz1 = (B.bmax[2] - o.z) * inv.z;
-    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
-    return !(tn > tf);
-}
-__device__ __forceinline__ v3 rcp3(v3 d) {
-    return mk(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
-}
-
 // Small triangle scenes (<= kSmallTris triangles, e.g. the Cornell box): every triangle
 // and the per-object boxes live in LDS for the whole launch; objects are visited in
 // Scene iteration order and a wave skips an object none of its rays can hit (closest-hit
@@ -508,148 +296,6 @@ __global__ __launch_bounds__(kBlock) void k_trace_small(KParams P, const uint32_
             if (smask) P.occ[s] = occ;
         }
     }
-}
-
-// =================================================================== shading ====
-struct Surf {
-    v3 pos, ng, ns, dpdu, dpdv;
-    int obj;
-};
-
-__device__ __forceinline__ v3 tri_ns(const KParams& P, int i, float u, float v) {
-    const float w = 1.0f - u - v;
-    return xyz(P.tri_nrm[3 * i]) * w + xyz(P.tri_nrm[3 * i + 1]) * u + xyz(P.tri_nrm[3 * i + 2]) * v;
-}
-
-// Rebuild IntersectInfo::surfaceInfo as Scene::intersect leaves it (Src/primitive.cpp:
-// 102-110, primitive.h:112-122).  Returns the hit object index (-1 = miss).
-template <int SCN>
-__device__ __forceinline__ int surface(const KParams& P, uint32_t s, v3 o, v3 d, f4 h, Surf& S, float& t1) {
-    const int code = __float_as_int(h.w);
-    S.pos = S.ng = S.ns = S.dpdu = S.dpdv = mk(0, 0, 0);
-    t1 = kINF;
-    if (code < 0) return -1;
-    int surf = code, dp = (SCN == SCN_TRI) ? code : -1;
-    float st = h.x, su = h.y, sv = h.z, du = h.y, dv = h.z;
-    if (SCN == SCN_MIXED) {
-        const f4 h2 = P.hit2[s], h3 = P.hit3[s];
-        t1 = h2.x;
-        surf = __float_as_int(h2.y), dp = __float_as_int(h2.z), st = h2.w;
-        su = h3.x, sv = h3.y, du = h3.z, dv = h3.w;
-    }
-    if (surf >= 0) {
-        const int kind = surf >> 28, idx = surf & 0x0fffffff;
-        S.pos = ray_at(o, d, st);
-        if (kind == SEG_TRI) {
-            S.ng = xyz(P.tri_ng[idx]);
-            S.ns = tri_ns(P, idx, su, sv);
-        } else {
-            S.ng = normalize(ray_at(o, d, st) - xyz(P.sph[idx]));
-            S.ns = S.ng;
-        }
-    }
-    if (dp >= 0) onb(tri_ns(P, dp & 0x0fffffff, du, dv), S.dpdu, S.dpdv);
-    const int kind = code >> 28, idx = code & 0x0fffffff;
-    if (kind == SEG_TRI) return __float_as_int(P.tri[3 * idx].w);
-    if (kind == SEG_SPHERE) return P.sph_obj[idx] & 0x3fffffff;
-    return __float_as_int(P.box[2 * idx].w);
-}
-
-// AreaLight::Le (Src/light.h:62-69)
-__device__ __forceinline__ v3 light_Le(const DLight& L, v3 ns, v3 wi) {
-    return dot(wi, ns) < 0.0f ? mk(L.Le[0], L.Le[1], L.Le[2]) : mk(0, 0, 0);
-}
-
-__device__ __forceinline__ v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
-
-// QuadLight::sample (Src/light.cpp:59-68; first draw scales e2 under GCC),
-// TriangleLight::sample (light.cpp:21-30,43-47; first draw is v),
-// SphereLight::sample default branch (light.h:157-197).  pdf is left untouched on the
-// back-facing early return, as in the reference.
-__device__ v3 light_sample(const DLight& L, v3 x, v3& wi, float& pdf, float& tmax, Rng& rng) {
-    if (L.kind == 0) {
-        const float ra = rng.next();
-        const float rb = rng.next();
-        const v3 dd = ((ld3(L.v0) + ld3(L.e1) * rb) + ld3(L.e2) * ra) - x;
-        tmax = length(dd);
-        const float dn = dot(dd, ld3(L.Ng));
-        if (dn >= 0.0f) return mk(0, 0, 0);
-        wi = dd / tmax;
-        pdf = (tmax * tmax * tmax) / __builtin_fabsf(dn);
-        return ld3(L.Le);
-    } else if (L.kind == 1) {
-        const float vv = rng.next();
-        const float uu = rng.next();
-        const float su = __builtin_sqrtf(uu);
-        const v3 A = ld3(L.v0), B = ld3(L.v1), C = ld3(L.v2);
-        const v3 p = (C + (A - C) * (1.0f - su)) + (B - C) * (vv * su);
-        const v3 dd = p - x;
-        tmax = length(dd);
-        const float dn = dot(dd, ld3(L.Ng));
-        if (dn >= 0.0f) return mk(0, 0, 0);
-        wi = dd / tmax;
-        pdf = (2.0f * tmax * tmax * tmax) / __builtin_fabsf(dn);
-        return ld3(L.Le);
-    }
-    const v3 center = ld3(L.center);
-    const float radius = L.radius;
-    v3 dz = center - x;
-    const float dz_len_2 = dot(dz, dz);
-    const float dz_len = __builtin_sqrtf(dz_len_2);
-    dz = dz / mk(-dz_len, -dz_len, -dz_len);
-    v3 dx, dy;
-    onb(dz, dx, dy);
-    const float sin_theta_max_2 = radius * radius / dz_len_2;
-    const float sin_theta_max = __builtin_sqrtf(sin_theta_max_2);
-    const float cos_theta_max = __builtin_sqrtf(smax(0.f, 1.f - sin_theta_max_2));
-    const float cos_theta = 1.0f + (cos_theta_max - 1.0f) * rng.next();
-    const float sin_theta_2 = 1.f - cos_theta * cos_theta;
-    const float cos_alpha =
-        sin_theta_2 / sin_theta_max + cos_theta * __builtin_sqrtf(smax(0.0f, 1.0f - sin_theta_2 / sin_theta_max_2));
-    const float sin_alpha = __builtin_sqrtf(smax(0.0f, 1.0f - cos_alpha * cos_alpha));
-    const float phi = kPI_MUL_2 * rng.next();
-    const v3 nn = (dx * (glibc_cosf(phi) * sin_alpha) + dy * (glibc_sinf(phi) * sin_alpha)) + dz * cos_alpha;
-    const v3 p = center + nn * radius;
-    const v3 dd = p - x;
-    tmax = length(dd);
-    if (dot(dd, nn) >= 0.0f) return mk(0, 0, 0);
-    pdf = 1.f / (kPI_MUL_2 * (1.f - cos_theta_max));
-    wi = dd / tmax;
-    return ld3(L.Le);
-}
-
-// Lambert::sampleDir + uniformSampleHemisphere (Src/material.h:55-73)
-__device__ __forceinline__ v3 lambert_sample_f(v3 ng, v3 dpdu, v3 dpdv, Rng& rng) {
-    const float r1 = rng.next();
-    const float r2 = rng.next();
-    const float sinTheta = __builtin_sqrtf(1.0f - r1 * r1);
-    const float phi = 2.0f * kPI * r2;
-    const float x = sinTheta * glibc_cosf(phi);
-    const float z = sinTheta * glibc_sinf(phi);
-    return local_to_world(mk(x, r1, z), dpdu, ng, dpdv);
-}
-__device__ __forceinline__ v3 lambert_sample(const Surf& S, Rng& rng) {
-    const float r1 = rng.next();
-    const float r2 = rng.next();
-    const float sinTheta = __builtin_sqrtf(1.0f - r1 * r1);
-    const float phi = 2.0f * kPI * r2;
-    const float x = sinTheta * glibc_cosf(phi);
-    const float z = sinTheta * glibc_sinf(phi);
-    return local_to_world(mk(x, r1, z), S.dpdu, S.ng, S.dpdv);
-}
-
-__device__ __forceinline__ v3 eval_bxdf(const DObj& ob) {   // Lambert::evaluateBxDF
-    return ob.material == 1 ? ld3(ob.albedo) / kPI : mk(0, 0, 0);
-}
-
-// PinholeCamera::sampleRay (Src/camera.h:49-60)
-__device__ __forceinline__ void camera_ray(const KParams& P, float u, float v, v3& o, v3& d) {
-    const v3 dir = mk((2.0f * u - 1.0f) * P.scale, (1.0f - 2.0f * v) * P.scale / P.aspect, -1.0f);
-    const float* x = P.c2w;
-    const v3 w = mk(dir.x * x[0] + dir.y * x[4] + dir.z * x[8], dir.x * x[1] + dir.y * x[5] + dir.z * x[9],
-                    dir.x * x[2] + dir.y * x[6] + dir.z * x[10]);
-    d = normalize(w);
-    o = mk(x[12], x[13], x[14]);
 }
 
 // ==================================================================== medium ====
@@ -1079,49 +725,6 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
     }
 }
 
-// LDS carve of the fused schedule (bytes; every f4 region 16-aligned): triangles, their
-// geometric and vertex normals, per-object culling boxes (triangle scenes), spheres,
-// medium boxes, the object and light tables, sphere->object map.
-struct StepLayout {
-    uint32_t tri, tng, nrm, box, sph, bx, obj, light, sobj, total;
-};
-__host__ __device__ inline StepLayout step_layout(const KParams& P) {
-    StepLayout L;
-    L.tri = 0;
-    L.tng = L.tri + 48u * P.n_tris;
-    L.nrm = L.tng + 16u * P.n_tris;
-    L.box = L.nrm + 48u * P.n_tris;
-    L.sph = L.box + (P.scene_kind == SCN_TRI ? 32u * P.n_objs : 0u);
-    L.bx = L.sph + 16u * P.n_sph;
-    L.obj = L.bx + 32u * P.n_box;
-    L.light = L.obj + (uint32_t)sizeof(DObj) * P.n_objs;
-    L.sobj = L.light + (uint32_t)sizeof(DLight) * P.n_lights;
-    L.total = L.sobj + 4u * P.n_sph;
-    return L;
-}
-
-// ============================================================ fused schedule ====
-// k_step: per live slot, up to `visits` path segments in one launch with the path state in
-// registers: trace the pending ray, shade the hit (NEE shadow rays traced immediately, so
-// no shadow state crosses a segment), finish/regenerate samples — the per-pixel sequence
-// of NormalRenderer::doRender + integrate().  The scene and its tables live in LDS
-// (step_layout), so this schedule serves scenes up to kStepLds bytes (C1, C2, C3, C5);
-// larger scenes use the multi-pass wavefront (k_shade / k_trace with LDS tiles).  A slot
-// stops early when its RNG ring runs low or it is done; at the end of the launch the slot
-// is appended to the next round's live list and, when fewer than rng_keep words are left,
-// to the refill list k_refill services between rounds.
-struct LScene {
-    const f4* tri;      // 3 per triangle
-    const f4* tng;      // geometric normal per triangle
-    const f4* nrm;      // 3 vertex normals per triangle
-    const DObjBox* box; // per object (SCN_TRI)
-    const f4* sph;
-    const int* sobj;
-    const f4* bx;       // 2 per box
-    const DObj* obj;
-    const DLight* light;
-};
-
 // Debug instrumentation (-DXRT_COUNT_TESTS, experiment builds only): triangle tests done
 // per lane and per wave (a wave pays for an object when any of its lanes needs it).
 #ifdef XRT_COUNT_TESTS
@@ -1137,6 +740,31 @@ struct LScene {
 #define CNT_ARG
 #define CNT_OBJ(ne, n) \
     do {               \
+    } while (0)
+#endif
+
+// Debug instrumentation (-DXRT_PHASE_CLOCK, experiment builds only): s_memtime cycles per
+// k_step_tri phase, summed over waves (lane 0) into stats[8 + phase].
+#ifdef XRT_PHASE_CLOCK
+#define PH_DECL uint64_t ph_t = __builtin_amdgcn_s_memtime(); uint64_t ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PH_MARK(i)                                            \
+    do {                                                      \
+        const uint64_t ph_n = __builtin_amdgcn_s_memtime();   \
+        ph_acc[i] += ph_n - ph_t;                             \
+        ph_t = ph_n;                                          \
+    } while (0)
+#define PH_FLUSH                                                                     \
+    do {                                                                             \
+        if (lane == 0)                                                               \
+            for (int q = 0; q < 8; ++q) atomicAdd(P.stats + 8 + q, (unsigned long long)ph_acc[q]); \
+    } while (0)
+#else
+#define PH_DECL
+#define PH_MARK(i) \
+    do {           \
+    } while (0)
+#define PH_FLUSH \
+    do {         \
     } while (0)
 #endif
 
@@ -1247,11 +875,6 @@ __device__ __forceinline__ bool occluded_l(const KParams& P, const LScene& L, v3
     }
 }
 
-__device__ __forceinline__ v3 tri_ns_l(const LScene& L, int i, float u, float v) {
-    const float w = 1.0f - u - v;
-    return xyz(L.nrm[3 * i]) * w + xyz(L.nrm[3 * i + 1]) * u + xyz(L.nrm[3 * i + 2]) * v;
-}
-
 // IntersectInfo::surfaceInfo from a hit record (see surface<>)
 template <int SCN>
 __device__ __forceinline__ int surface_l(const LScene& L, v3 o, v3 d, const HitRec& h, Surf& S) {
@@ -1276,14 +899,6 @@ __device__ __forceinline__ int surface_l(const LScene& L, v3 o, v3 d, const HitR
     if (kind == SEG_TRI) return __float_as_int(L.tri[3 * idx].w);
     if (kind == SEG_SPHERE) return L.sobj[idx] & 0x3fffffff;
     return __float_as_int(L.bx[2 * idx].w);
-}
-
-template <typename T>
-__device__ __forceinline__ void lds_copy(T* dst, const T* src, int n, int tid) {
-    const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
-    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
-    const int words = n * (int)(sizeof(T) / 4);
-    for (int q = tid; q < words; q += kBlock) d[q] = s[q];
 }
 
 #ifndef XRT_STEP_WAVES
@@ -1574,9 +1189,22 @@ struct CoopWave {
 constexpr int kCoopMaxObjs = 32;
 constexpr uint32_t kCoopCap = 512;
 
+#ifdef XRT_PHASE_CLOCK
+#define CT_PARAM , uint64_t* g_ct
+#define CT_ARGP , g_ct
+#else
+#define CT_PARAM
+#define CT_ARGP
+#endif
 template <bool SHADOW>
 __device__ __forceinline__ unsigned long long coop_trace(const KParams& P, const LScene& L, CoopWave& W, int lane,
-                                                         bool want, v3 o, v3 d, float tmax CNT_PARAM) {
+                                                         bool want, v3 o, v3 d, float tmax CNT_PARAM CT_PARAM) {
+#ifdef XRT_PHASE_CLOCK
+    uint64_t ct = __builtin_amdgcn_s_memtime();
+#define CT_MARK(q) do { const uint64_t cn = __builtin_amdgcn_s_memtime(); g_ct[(SHADOW ? 4 : 0) + q] += cn - ct; ct = cn; } while (0)
+#else
+#define CT_MARK(q) do {} while (0)
+#endif
     uint32_t m = 0, n = 0;
     if (want) {
         const v3 inv = rcp3(d);
@@ -1589,6 +1217,7 @@ __device__ __forceinline__ unsigned long long coop_trace(const KParams& P, const
 #ifdef XRT_COUNT_TESTS
     cnt_l += n;
 #endif
+    CT_MARK(0);
     uint32_t incl = n;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -1600,6 +1229,7 @@ __device__ __forceinline__ unsigned long long coop_trace(const KParams& P, const
     W.ro[lane] = make_float4(o.x, o.y, o.z, tmax);
     W.rd[lane] = make_float4(d.x, d.y, d.z, 0.0f);
     W.best[lane] = SHADOW ? 0ull : ~0ull;
+    CT_MARK(1);
 #ifdef XRT_COUNT_TESTS
     cnt_w += (total + 63) / 64 * 64;
 #endif
@@ -1618,6 +1248,7 @@ __device__ __forceinline__ unsigned long long coop_trace(const KParams& P, const
             }
         }
         wave_sync();
+        CT_MARK(2);
         const uint32_t cnt = min(kCoopCap, total - c0);
         for (uint32_t j = lane; j < cnt; j += 64) {
             const uint32_t e = W.pair[j];
@@ -1634,13 +1265,15 @@ __device__ __forceinline__ unsigned long long coop_trace(const KParams& P, const
             }
         }
         wave_sync();
+        CT_MARK(3);
     }
+#undef CT_MARK
     return W.best[lane];
 }
 
 __device__ __forceinline__ void coop_closest(const KParams& P, const LScene& L, CoopWave& W, int lane, bool want, v3 o,
-                                             v3 d, HitRec& h CNT_PARAM) {
-    const unsigned long long b = coop_trace<false>(P, L, W, lane, want, o, d, kINF CNT_ARG);
+                                             v3 d, HitRec& h CNT_PARAM CT_PARAM) {
+    const unsigned long long b = coop_trace<false>(P, L, W, lane, want, o, d, kINF CNT_ARG CT_ARGP);
     h.t = kINF, h.u = h.v = 0.0f, h.code = -1, h.surf = -1, h.dp = -1, h.t1 = kINF;
     h.st = h.su = h.sv = h.du = h.dv = 0.0f;
     if (want && b != ~0ull) {
@@ -1678,6 +1311,12 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
     L.light = reinterpret_cast<const DLight*>(lb + Lo.light);
     L.sobj = reinterpret_cast<const int*>(lb + Lo.sobj);
     const int tid = threadIdx.x, lane = tid & 63;
+#ifdef XRT_PHASE_CLOCK
+    const uint64_t kt0 = __builtin_amdgcn_s_memtime(), kr0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t kt1 = 0;
+    uint32_t ph_vis = 0;
+    uint64_t g_ct[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     CoopWave& W = reinterpret_cast<CoopWave*>(lb + ((Lo.total + 15u) & ~15u))[tid >> 6];
     lds_copy(const_cast<f4*>(L.tri), P.tri, 3 * P.n_tris, tid);
     lds_copy(const_cast<f4*>(L.tng), P.tri_ng, P.n_tris, tid);
@@ -1688,6 +1327,9 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
     __syncthreads();
     zero_parts(P, zero_count);
     const PartIter it = part_iter(P, count, kBlock);
+#ifdef XRT_PHASE_CLOCK
+    kt1 = __builtin_amdgcn_s_memtime();
+#endif
     for (uint32_t base = it.first; base < it.n; base += it.stride) {
         const uint32_t i = base + tid;
         const uint32_t s = i < it.n ? list[it.p * P.part_cap + i] : 0;
@@ -1714,6 +1356,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
             rng.prefetch(g - rng.c);
         }
         uint32_t nseg = 0, nsh = 0, nrej = 0;
+        PH_DECL
         for (uint32_t vis = 0; vis < visits; ++vis) {
             const bool act = live && !(st & ST_DONE) && g - rng.c >= kRngVisit;
             if (!__ballot(act)) break;
@@ -1730,7 +1373,9 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
             if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) ended = act;   // bounce loop never runs
             const bool ext = act && !ended;
             HitRec h;
-            coop_closest(P, L, W, lane, ext, o, d, h CNT_ARG);
+            PH_MARK(0);
+            coop_closest(P, L, W, lane, ext, o, d, h CNT_ARG CT_ARGP);
+            PH_MARK(1);
             // SurfaceInfo of a triangle hit: position, face normal; the shading normal (for
             // Le) and the dpdu/dpdv frame (for the BSDF) are rebuilt from (tri, u, v) where used
             Surf S;
@@ -1776,6 +1421,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
                     }
                 }
             }
+            PH_MARK(2);
             // next-event estimation: one cooperative shadow trace per light, in light order
             v3 directL = mk(0, 0, 0);
             for (int l = 0; l < P.n_lights; ++l) {
@@ -1784,7 +1430,9 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
                 if (alive) Lv = light_sample(L.light[l], S.pos, wi, pdf, tmax, rng);
                 const bool sh = alive && pdf != 0.0f;
                 const float bias = 0.01f;
-                const bool occ = coop_trace<true>(P, L, W, lane, sh, S.pos + S.ng * bias, wi, tmax - bias CNT_ARG) != 0;
+                PH_MARK(3);
+                const bool occ = coop_trace<true>(P, L, W, lane, sh, S.pos + S.ng * bias, wi, tmax - bias CNT_ARG CT_ARGP) != 0;
+                PH_MARK(4);
                 if (sh) {
                     ++nsh;
                     const float cosv = smax(0.0f, dot(S.ng, wi));
@@ -1798,6 +1446,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
                     }
                 }
             }
+            PH_MARK(3);
             if (alive) {
                 if (INTEG == XRT_INTEGRATOR_DIRECT) {
                     ended = true;
@@ -1821,6 +1470,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
                     if (depth >= P.max_depth) ended = true;
                 }
             }
+            PH_MARK(5);
             // finish the sample and start the next one (see k_step)
             while (ended) {
                 ended = false;
@@ -1846,8 +1496,14 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
                     depth = 0;
                 }
             }
+            PH_MARK(6);
             if (act) rng.prefetch(g - rng.c);
+            PH_MARK(7);
+#ifdef XRT_PHASE_CLOCK
+            ++ph_vis;
+#endif
         }
+        PH_FLUSH;
         bool want_req = false;
         if (live) {
             px[0] = acc.x, px[1] = acc.y, px[2] = acc.z;
@@ -1877,6 +1533,22 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
         wave_append(live && !(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
         wave_append(want_req, s, P.req + it.p * P.part_cap, req_count + it.p, lane);
     }
+#ifdef XRT_PHASE_CLOCK
+    if (lane == 0) {
+        atomicAdd(P.stats + 16, (unsigned long long)(__builtin_amdgcn_s_memtime() - kt0));
+        atomicAdd(P.stats + 17, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - kr0));
+        atomicAdd(P.stats + 18, 1ull);
+        atomicAdd(P.stats + 19, (unsigned long long)(kt1 - kt0));
+        if (ph_vis) {
+            const unsigned long long life = __builtin_amdgcn_s_memtime() - kt0;
+            atomicAdd(P.stats + 20, (unsigned long long)ph_vis);
+            atomicMax(P.stats + 21, life);
+            atomicAdd(P.stats + 22, life);
+            atomicAdd(P.stats + 23, 1ull);
+        }
+        for (int q = 0; q < 8; ++q) atomicAdd(P.stats + 24 + q, (unsigned long long)g_ct[q]);
+    }
+#endif
 }
 
 // ================================================================== k_finish ====

@@ -19,6 +19,8 @@
 
 using namespace xrt;
 
+static constexpr float kPiF = 3.14159265359;   // Src/geometry.h:10 (float PI), = device_math.h kPI
+
 namespace {
 
 struct DevBuf {
@@ -36,6 +38,7 @@ struct xrt_ctx {
     std::vector<DevBuf*> scene_bufs;
     DevBuf tri, tri_ng, tri_nrm, sph, sph_obj, box, objs, lights, segs, density, obj_box;
     KParams base{};
+    StepObjs step_objs{};   // kernel-argument object records of the merged-trace schedule
     bool has_scene = false, has_camera = false, has_medium = false;
     // slots
     size_t cap_slots = 0;
@@ -167,7 +170,7 @@ int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
             return set_err(c, XRT_ERR_INVALID, "object " + std::to_string(k) + ": bad light index or range");
         DObj d{};
         d.kind = o.kind, d.material = o.material, d.light = o.light, d.medium = o.medium;
-        for (int q = 0; q < 3; ++q) d.albedo[q] = o.albedo[q];
+        for (int q = 0; q < 3; ++q) d.fr[q] = o.material == 1 ? o.albedo[q] / kPiF : 0.0f;
         objs.push_back(d);
         const bool occluder = o.light < 0;  // Scene::occluded skips area-light objects
         int kind = -1, first = 0;
@@ -285,6 +288,7 @@ int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
             for (int q = 0; q < 3; ++q) b.bmin[q] -= margin, b.bmax[q] += margin;
         if ((rc = upload(c, c->obj_box, boxes.data(), boxes.size() * sizeof(DObjBox)))) return rc;
         P.obj_box = as<DObjBox>(c->obj_box);
+        if (boxes.size() <= (size_t)kMergedMaxObjs) build_step_objs(boxes.data(), (int)boxes.size(), c->step_objs);
         P.small_tri = 1;
     }
     c->has_scene = true;
@@ -359,7 +363,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             return rc;
         c->cap_slots = n;
     }
-    if ((rc = ensure(c, c->counts, 5 * kMaxParts * 4)) || (rc = ensure(c, c->stats, 64))) return rc;
+    if ((rc = ensure(c, c->counts, 5 * kMaxParts * 4)) || (rc = ensure(c, c->stats, 256))) return rc;
     float* fb = d_out;
     if (!fb) {
         if ((rc = ensure(c, c->fb, npix * 3 * sizeof(float)))) return rc;
@@ -423,7 +427,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     };
 
     HIPCHK(c, hipMemsetAsync(fb, 0, npix * 3 * sizeof(float), c->stream));
-    HIPCHK(c, hipMemsetAsync(P.stats, 0, 64, c->stream));
+    HIPCHK(c, hipMemsetAsync(P.stats, 0, 256, c->stream));
     HIPCHK(c, launch(XRT_K_SEED, [&] { return launch_seed(P, lists[0], counts_at(0), counts_at(1), req_counts, c->stream); }));
     // refill epochs: shading launches of epoch e append to req_counts[e & 1]; k_refill(e)
     // consumes it and clears req_counts[(e + 1) & 1] for epoch e + 1.  Epoch 0 is the
@@ -464,11 +468,15 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     // iterations).  k_step rotates three live counters: round i reads counts[i%3], appends
     // to counts[(i+1)%3] and clears counts[(i+2)%3] for round i+1.
     const bool fused = !(p->flags & XRT_FLAG_WAVEFRONT) && step_lds_bytes(P) != 0;
+    const bool merged = fused && !(p->flags & XRT_FLAG_NO_MERGED) && use_step_merged(P);
     // tuning knobs (defaults kStepVisits / kStepRefill; XRT_STEP_VISITS / XRT_STEP_REFILL
     // override them for experiments — results do not depend on them)
-    const uint32_t step_visits = env_u32("XRT_STEP_VISITS", kStepVisits, 1, 64);
+    const uint32_t step_visits = env_u32("XRT_STEP_VISITS", merged ? kMergedVisits : kStepVisits, 1, 128);
     const uint32_t step_refill = env_u32("XRT_STEP_REFILL", kStepRefill, 1, 8);
-    P.rng_keep = step_refill * step_visits * kVisitDraws + kRngVisit;
+    // a slot queues a refill when fewer words are left than the next `refill` launches can
+    // draw: the merged kernel draws at most step_merged_draws per segment and checks it
+    P.rng_keep = merged ? step_refill * step_visits * step_merged_draws(P) + step_merged_draws(P)
+                        : step_refill * step_visits * kVisitDraws + kRngVisit;
     if (P.rng_keep > kMT) return set_err(c, XRT_ERR_INVALID, "XRT_STEP_VISITS * XRT_STEP_REFILL too large");
     // device copy of the (now final) parameters for kernels that read them from memory
     if ((rc = ensure(c, c->kparams, sizeof(KParams)))) return rc;
@@ -482,6 +490,10 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             const int ci = (int)(it % 3), co = (int)((it + 1) % 3), cz = (int)((it + 2) % 3);
             live = counts_at(co);
             hipError_t e = launch(XRT_K_STEP, [&] {
+                if (merged)
+                    return launch_step_merged(P, dP, c->step_objs, lists[cur], counts_at(ci), lists[nxt],
+                                              counts_at(co), counts_at(cz), req_counts + (epoch & 1) * kMaxParts,
+                                              step_visits, blocks, c->stream);
                 return launch_step(P, dP, lists[cur], counts_at(ci), lists[nxt], counts_at(co), counts_at(cz),
                                    req_counts + (epoch & 1) * kMaxParts, step_visits, blocks, c->stream);
             });
@@ -537,11 +549,22 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
         for (uint32_t k = 0; k < P.n_part; ++k)
             if (left[k] != 0) return set_err(c, XRT_ERR_HIP, "iteration cap reached with live paths");
     }
-    unsigned long long hs[8] = {0};
-    HIPCHK(c, hipMemcpy(hs, P.stats, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long hs[32] = {0};
+    HIPCHK(c, hipMemcpy(hs, P.stats, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     if (hs[5] || hs[6]) std::fprintf(stderr, "[xrt] triangle tests: lane %llu wave %llu\n", hs[5], hs[6]);
+    if (hs[8] || hs[9]) {   // -DXRT_PHASE_CLOCK experiment builds
+        std::fprintf(stderr, "[xrt] phase cycles (sum over waves):");
+        for (int q = 8; q < 16; ++q) std::fprintf(stderr, " %llu", hs[q]);
+        std::fprintf(stderr, " | kernel memtime %llu realtime %llu waves %llu prologue %llu | visit iters %llu max life %llu busy life %llu busy waves %llu",
+                     hs[16], hs[17], hs[18], hs[19], hs[20], hs[21], hs[22], hs[23]);
+        std::fprintf(stderr, " | coop closest cull/scan/expand/pass %llu %llu %llu %llu shadow %llu %llu %llu %llu",
+                     hs[24], hs[25], hs[26], hs[27], hs[28], hs[29], hs[30], hs[31]);
+        std::fprintf(stderr, "\n");
+    }
     S.segments = hs[0], S.shadow_rays = hs[1], S.draws = hs[2], S.rejected = hs[3], S.stalled = hs[4];
-    S.schedule = !fused ? XRT_SCHED_WAVEFRONT : use_step_tri(P) ? XRT_SCHED_STEP_TRI : XRT_SCHED_STEP;
+    S.schedule = !fused ? XRT_SCHED_WAVEFRONT
+                 : merged ? XRT_SCHED_STEP_MERGED
+                 : use_step_tri(P) ? XRT_SCHED_STEP_TRI : XRT_SCHED_STEP;
     if (timing) {
         for (auto& u : ev_use) {
             float ms = 0.0f;

@@ -52,16 +52,19 @@ class HipRenderer:
 
     def params(self, scene, width, height, shard_index=0, shard_count=1, timing=False, integrator=None,
                max_depth=None, schedule="auto"):
-        """schedule: "auto" (fused k_step when the scene fits in LDS, else the multi-pass
-        wavefront) or "wavefront" (always k_shade + k_trace)."""
-        if schedule not in ("auto", "wavefront"):
+        """schedule: "auto" (fused k_step when the scene fits in LDS — for small triangle
+        scenes with merged shadow + extension traces — else the multi-pass wavefront),
+        "wavefront" (always k_shade + k_trace) or "step_tri" (fused, one cooperative trace
+        per ray kind instead of the merged traces)."""
+        if schedule not in ("auto", "wavefront", "step_tri"):
             raise ValueError(f"unknown schedule {schedule!r}")
         p = abi.XrtRenderParams()
         p.integrator = abi.INTEGRATORS[integrator or scene.integrator]
         p.max_depth = scene.max_depth if max_depth is None else max_depth
         p.width, p.height, p.spp = width, height, self.spp
         p.shard_index, p.shard_count = shard_index, shard_count
-        p.flags = (abi.XRT_FLAG_TIMING if timing else 0) | (abi.XRT_FLAG_WAVEFRONT if schedule == "wavefront" else 0)
+        p.flags = ((abi.XRT_FLAG_TIMING if timing else 0) | (abi.XRT_FLAG_WAVEFRONT if schedule == "wavefront" else 0) |
+                   (abi.XRT_FLAG_NO_MERGED if schedule == "step_tri" else 0))
         return p
 
     def render(self, scene: SceneBundle, width: int, height: int, **kw) -> np.ndarray:
