@@ -208,11 +208,14 @@ def test_merged_segments_per_launch(renderer, visits, monkeypatch):
         assert (g.segments, g.shadow_rays, g.draws) == (st["segments"], st["shadow_rays"], st["draws"])
 
 
-@pytest.mark.parametrize("spw", [16, 32, 64])
-def test_merged_slots_per_wave(renderer, spw, monkeypatch):
-    """Half- and quarter-filled waves (the merged kernel's layout for small pixel shards)
-    render the same image and counters as full waves."""
+@pytest.mark.parametrize("spw,group", [(16, True), (32, True), (64, True), (16, False), (32, False)])
+def test_merged_slots_per_wave(renderer, spw, group, monkeypatch):
+    """The merged kernel's layouts for small pixel shards — 16 or 32 slots per wave, their
+    traces shared by 4 or 2 lanes per slot (group trace) or spread over idle lanes
+    (cooperative passes) — render the same image and counters as full waves."""
     monkeypatch.setenv("XRT_MERGED_SPW", str(spw))
+    if not group:
+        monkeypatch.setenv("XRT_NO_GROUP", "1")
     s = scenes.cornell(40, 30)
     for kw in ({}, {"integrator": "direct"}):
         img, ref, st = render_both(renderer, s, 40, 30, 5, **kw)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/regs.sh [pattern] — per-kernel VGPR/SGPR/spill/occupancy of wavefront.hip (gfx950)
 cd "$(dirname "$0")/../xraytracer_amd/csrc"
-/opt/rocm/bin/hipcc -O3 -std=c++17 -ffp-contract=off -I../../include -I. --offload-arch=gfx950 \
+/opt/rocm/bin/hipcc -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -I../../include -I. --offload-arch=gfx950 \
     $REGS_DEFS -c wavefront.hip -o /tmp/regs_wf.o -Rpass-analysis=kernel-resource-usage 2>&1 |
 python3 -c '
 import re, sys

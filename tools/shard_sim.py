@@ -21,6 +21,7 @@ def main():
 
     cfg_name = sys.argv[1] if len(sys.argv) > 1 else "C2"
     timing = "--timing" in sys.argv
+    only = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--only=")]
     cfg = scenes.CONFIGS[cfg_name]
     W, H, SPP = cfg["width"], cfg["height"], cfg["spp"]
     scene = scenes.build(cfg_name)
@@ -29,9 +30,9 @@ def main():
     fb = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0")
     r.render_device(scene, W, H, fb.data_ptr(), shard_index=0, shard_count=8)  # warm
     res = {}
-    for n in (1, 2, 4, 8):
+    for n in (only or (1, 2, 4, 8)):
         times = []
-        for s in sorted({0, n - 1}):
+        for s in (sorted({0, n - 1}) if not only else [0]):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             st = r.render_device(scene, W, H, fb.data_ptr(), shard_index=s, shard_count=n, timing=timing)

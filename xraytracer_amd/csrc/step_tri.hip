@@ -115,7 +115,11 @@ template <int NL>
 __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L, MergedWave<NL>& W, int lane,
                                              bool ext, v3 o, v3 d, uint32_t shm, const v3 (&so)[NL + 1],
                                              const v3 (&sd)[NL + 1], const float (&stm)[NL + 1],
-                                             unsigned long long& best, uint32_t& occ) {
+                                             unsigned long long& best, uint32_t& occ
+#ifdef XRT_PHASE_CLOCK
+                                             , uint64_t* ph_acc, uint32_t* ph_cnt
+#endif
+) {
     constexpr int R = 1 + NL;
     W.best[lane] = ~0ull;
     W.occ[lane] = 0u;
@@ -128,7 +132,7 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
     wave_sync();
     const int n = SO.n;
     for (int ob = 0; ob < n; ++ob) {
-        const StepObj& B = SO.o[ob];
+        const StepObj B = SO.o[ob];
         bool need[R];
         need[0] = ext && obj_overlap(o, inv[0], B, kINF);
 #pragma unroll
@@ -145,6 +149,9 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
         wave_sync();
         const uint32_t c = B.count, first = (uint32_t)B.first, magic = B.magic;
         const uint32_t pairs = tot * c;
+#ifdef XRT_PHASE_CLOCK
+        ph_cnt[0] += (pairs + 63) / 64, ph_cnt[1] += pairs, ph_cnt[2] += 1;
+#endif
         for (uint32_t j0 = 0; j0 < pairs; j0 += 64) {
             const uint32_t j = j0 + (uint32_t)lane;
             if (j < pairs) {
@@ -170,7 +177,93 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
     occ = W.occ[lane];
 }
 
+// Group trace (G = 2 or 4 lanes per slot, scenes of <= 64 triangles): the G lanes of a
+// slot hold identical path state (every shading instruction runs on all of them) and split
+// its traces among themselves, with no LDS traffic but the triangle fetches: lane u culls
+// objects u, u+G, ... into 64-bit triangle masks (one per ray), the masks are OR-ed across
+// the group by DPP, lane u tests the candidate triangles k = u (mod G) in increasing k, and
+// the group reduces by DPP: min of (t bits << 32 | k) for the extension ray — smallest t,
+// then lowest index, the reference's in-order `t < best` scan — and OR of occlusion bits.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, false);
+}
+template <int G>
+__device__ __forceinline__ uint32_t group_or32(uint32_t x) {
+    if (G >= 2) x |= dpp32<0xB1>(x);   // quad_perm(1, 0, 3, 2): partner lane ^ 1
+    if (G >= 4) x |= dpp32<0x4E>(x);   // quad_perm(2, 3, 0, 1): partner lane ^ 2
+    return x;
+}
+template <int G>
+__device__ __forceinline__ uint64_t group_or64(uint64_t x) {
+    return ((uint64_t)group_or32<G>((uint32_t)(x >> 32)) << 32) | group_or32<G>((uint32_t)x);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t min64_dpp(uint64_t x) {
+    const uint64_t y = ((uint64_t)dpp32<CTRL>((uint32_t)(x >> 32)) << 32) | dpp32<CTRL>((uint32_t)x);
+    return y < x ? y : x;
+}
+template <int G>
+__device__ __forceinline__ uint64_t group_min64(uint64_t x) {
+    if (G >= 2) x = min64_dpp<0xB1>(x);
+    if (G >= 4) x = min64_dpp<0x4E>(x);
+    return x;
+}
+
+template <int NL, int G>
+__device__ __forceinline__ void group_trace(int n_objs, const LScene& L, int lane, bool ext, v3 o, v3 d,
+                                            uint32_t shm, const v3 (&so)[NL + 1], const v3 (&sd)[NL + 1],
+                                            const float (&stm)[NL + 1], unsigned long long& best, uint32_t& occ) {
+    constexpr int R = 1 + NL;
+    const int u = lane & (G - 1);
+    uint64_t tm[R];
+    v3 inv[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) tm[q] = 0ull;
+    inv[0] = rcp3(d);
+#pragma unroll
+    for (int l = 0; l < NL; ++l) inv[1 + l] = rcp3(sd[l]);
+    for (int ob0 = 0; ob0 < n_objs; ob0 += G) {
+        const int ob = ob0 + u;
+        if (ob < n_objs) {
+            const DObjBox B = L.box[ob];
+            const uint32_t cnt = (uint32_t)(B.count_occ & 0x7fffffff);
+            const uint64_t bits = (cnt >= 64u ? ~0ull : ((1ull << cnt) - 1ull)) << B.first;
+            if (ext && box_overlap(o, inv[0], B, kINF)) tm[0] |= bits;
+#pragma unroll
+            for (int l = 0; l < NL; ++l)
+                if (B.count_occ < 0 && ((shm >> l) & 1u) && box_overlap(so[l], inv[1 + l], B, stm[l])) tm[1 + l] |= bits;
+        }
+    }
+    const uint64_t pat = (G == 4 ? 0x1111111111111111ull : G == 2 ? 0x5555555555555555ull : ~0ull) << u;
+    unsigned long long bk = ~0ull;
+    for (uint64_t bits = group_or64<G>(tm[0]) & pat; bits; bits &= bits - 1ull) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(bits);
+        float t;
+        if (ray_tri_nb(o, d, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t)) {
+            const unsigned long long key = ((unsigned long long)__float_as_uint(t) << 32) | k;
+            bk = key < bk ? key : bk;
+        }
+    }
+    uint32_t oc = 0;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+        for (uint64_t bits = group_or64<G>(tm[1 + l]) & pat; bits; bits &= bits - 1ull) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(bits);
+            float t;
+            if (ray_tri_nb(so[l], sd[l], xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t) &&
+                t < stm[l]) {
+                oc |= 1u << l;
+                bits = 1ull;   // occluded: the loop update clears the rest
+            }
+        }
+    }
+    best = group_min64<G>(bk);
+    occ = group_or32<G>(oc);
+}
+
 #ifdef XRT_PHASE_CLOCK
+#define PH_TARGS , ph_acc, ph_cnt
 #define MPH_DECL uint64_t ph_t = __builtin_amdgcn_s_memtime();
 #define MPH_MARK(i)                                          \
     do {                                                     \
@@ -179,6 +272,7 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
         ph_t = ph_n;                                         \
     } while (0)
 #else
+#define PH_TARGS
 #define MPH_DECL
 #define MPH_MARK(i) \
     do {            \
@@ -189,11 +283,14 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
 #define XRT_STEP_WAVES 4
 #endif
 
-// SPW: path slots per wave (64, 32 or 16).  Lanes >= SPW own no slot but take part in
-// every pair pass of the cooperative traces, so a half- or quarter-filled wave traces its
-// rays in proportionally fewer passes; with few slots per GPU (a pixel shard of a
-// multi-GPU frame) this puts more, shorter waves on every SIMD.
-template <int INTEG, int NL, int SPW>
+// SPW: path slots per wave (64, 32 or 16), G: lanes per slot (1, or 64 / SPW for the group
+// trace).  With G = 1 and SPW < 64, lanes >= SPW own no slot but take part in every pair
+// pass of the cooperative traces, so a half- or quarter-filled wave traces its rays in
+// proportionally fewer passes; with G > 1 every lane of a slot's group runs its path
+// (redundantly, results identical) and the group shares the traces (group_trace).  Either
+// way, with few slots per GPU (a pixel shard of a multi-GPU frame) this puts more, shorter
+// waves on every SIMD.
+template <int INTEG, int NL, int SPW, int G>
 __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
     const KParams* __restrict__ Pp, const StepObjs SO, const uint32_t* __restrict__ list,
     const uint32_t* __restrict__ count, uint32_t* __restrict__ out, uint32_t* out_count, uint32_t* zero_count,
@@ -220,18 +317,20 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
     lds_copy(const_cast<f4*>(L.nrm), P.tri_nrm, 3 * P.n_tris, tid);
     lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
     lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid);
+    if (G > 1) lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid);
     __syncthreads();
 #ifdef XRT_PHASE_CLOCK
     uint64_t ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t ph_vis = 0;
+    uint32_t ph_vis = 0, ph_cnt[3] = {0, 0, 0};
     const uint64_t kt0 = __builtin_amdgcn_s_memtime();
 #endif
     zero_parts(P, zero_count);
     const PartIter it = part_iter(P, count, (kBlock / 64) * SPW);
     const uint32_t spp = P.spp, max_depth = P.max_depth, width = P.width, height = P.height;
     for (uint32_t base = it.first; base < it.n; base += it.stride) {
-        const uint32_t i = base + (uint32_t)(tid >> 6) * SPW + (uint32_t)lane;
-        const bool own = lane < SPW && i < it.n;
+        const uint32_t i = base + (uint32_t)(tid >> 6) * SPW + (uint32_t)lane / G;
+        const bool own = lane / G < SPW && i < it.n;
+        const bool lead = own && (lane % G) == 0;   // the lane of a group that writes back
         const uint32_t s = own ? list[it.p * P.part_cap + i] : 0;
         uint32_t st = own ? glb<gu32>(P.state)[s] : ST_DONE;
         const bool live = !(st & ST_DONE);
@@ -325,7 +424,10 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
             MPH_MARK(0);
             unsigned long long best;
             uint32_t occ;
-            merged_trace<NL>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
+            if constexpr (G == 1)
+                merged_trace<NL>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ PH_TARGS);
+            else
+                group_trace<NL, G>(P.n_objs, L, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
             MPH_MARK(1);
             resolve(occ);
             MPH_MARK(2);
@@ -387,8 +489,10 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                             shm |= 1u << l;
                             const float bias = 0.01f;
                             so[l] = pos + ng * bias, sd[l] = wi, stm[l] = tmax - bias;
-                            W.ro[(1 + l) * 64 + lane] = make_float4(so[l].x, so[l].y, so[l].z, stm[l]);
-                            W.rd[(1 + l) * 64 + lane] = make_float4(wi.x, wi.y, wi.z, 0.0f);
+                            if constexpr (G == 1) {
+                                W.ro[(1 + l) * 64 + lane] = make_float4(so[l].x, so[l].y, so[l].z, stm[l]);
+                                W.rd[(1 + l) * 64 + lane] = make_float4(wi.x, wi.y, wi.z, 0.0f);
+                            }
                             const float cosv = smax(0.0f, dot(ng, wi));
                             // vis * fr * L * cos / pdf (Src/integrator.h:250-262) for vis = 1, 0
                             c1[l] = (((fr * 1.0f) * Lv) * cosv) / pdf;
@@ -438,12 +542,15 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
         if (__ballot(shm != 0)) {
             unsigned long long best;
             uint32_t occ;
-            merged_trace<NL>(SO, L, W, lane, false, o, d, shm, so, sd, stm, best, occ);
+            if constexpr (G == 1)
+                merged_trace<NL>(SO, L, W, lane, false, o, d, shm, so, sd, stm, best, occ PH_TARGS);
+            else
+                group_trace<NL, G>(P.n_objs, L, lane, false, o, d, shm, so, sd, stm, best, occ);
             resolve(occ);
         }
         MPH_MARK(5);
         bool want_req = false;
-        if (live) {
+        if (live && lead) {
             px[0] = acc.x, px[1] = acc.y, px[2] = acc.z;
             want_req = !(st & (ST_DONE | ST_RNGREQ)) && g - rng.c < P.rng_keep;
             if (want_req) st |= ST_RNGREQ;
@@ -461,7 +568,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
             if (nsh) P.c_shadow[s] += nsh;
             if (nrej) P.c_rej[s] += nrej;
         }
-        wave_append(live && !(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
+        wave_append(live && lead && !(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
         wave_append(want_req, s, P.req + it.p * P.part_cap, req_count + it.p, lane);
     }
 #ifdef XRT_PHASE_CLOCK
@@ -469,6 +576,9 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
         for (int q = 0; q < 8; ++q) atomicAdd(P.stats + 8 + q, (unsigned long long)ph_acc[q]);
         atomicAdd(P.stats + 16, (unsigned long long)(__builtin_amdgcn_s_memtime() - kt0));
         atomicAdd(P.stats + 20, (unsigned long long)ph_vis);
+        atomicAdd(P.stats + 21, (unsigned long long)ph_cnt[0]);
+        atomicAdd(P.stats + 22, (unsigned long long)ph_cnt[1]);
+        atomicAdd(P.stats + 23, (unsigned long long)ph_cnt[2]);
     }
 #endif
 }
@@ -508,14 +618,14 @@ void build_step_objs(const DObjBox* boxes, int n, StepObjs& SO) {
     }
 }
 
-template <int INTEG, int SPW>
+template <int INTEG, int SPW, int G>
 static void launch_merged_i(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                             const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
                             uint32_t* req_count, uint32_t visits, size_t lds, hipStream_t st) {
     const uint32_t per_block = (kBlock / 64) * SPW;
     const uint32_t blocks = P.n_part * ((P.part_cap + per_block - 1) / per_block);
 #define XRT_LAUNCH_MERGED(NLV)                                                                                       \
-    hipLaunchKernelGGL((k_step_merged<INTEG, NLV, SPW>), dim3(blocks), dim3(kBlock), lds, st, dP, SO, list, count, \
+    hipLaunchKernelGGL((k_step_merged<INTEG, NLV, SPW, G>), dim3(blocks), dim3(kBlock), lds, st, dP, SO, list, count, \
                        out, out_count, zero, req_count, visits)
     switch (P.n_lights) {
         case 0: XRT_LAUNCH_MERGED(0); break;
@@ -543,11 +653,15 @@ template <int INTEG>
 static void launch_merged_spw(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                               const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
                               uint32_t* req_count, uint32_t visits, size_t lds, hipStream_t st) {
+    const bool group = P.n_tris <= 64 && !std::getenv("XRT_NO_GROUP");   // group trace: 64-bit triangle masks
+#define XRT_MERGED_CASE(SPWV, GV) \
+    launch_merged_i<INTEG, SPWV, GV>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, lds, st)
     switch (step_merged_spw(P)) {
-        case 64: launch_merged_i<INTEG, 64>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, lds, st); break;
-        case 32: launch_merged_i<INTEG, 32>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, lds, st); break;
-        default: launch_merged_i<INTEG, 16>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, lds, st); break;
+        case 64: XRT_MERGED_CASE(64, 1); break;
+        case 32: if (group) XRT_MERGED_CASE(32, 2); else XRT_MERGED_CASE(32, 1); break;
+        default: if (group) XRT_MERGED_CASE(16, 4); else XRT_MERGED_CASE(16, 1); break;
     }
+#undef XRT_MERGED_CASE
 }
 
 hipError_t launch_step_merged(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
