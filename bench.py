@@ -158,8 +158,8 @@ def main():
             avg_s = kms[dom] / 1e3 / launches
             achieved = per_launch / avg_s / 1e9
             kname = abi.KERNEL_NAMES[dom]
-            if dom == abi.XRT_K_STEP and sched == abi.XRT_SCHED_STEP_TRI:
-                kname = "step_tri"
+            if dom == abi.XRT_K_STEP and sched in (abi.XRT_SCHED_STEP_TRI, abi.XRT_SCHED_STEP_MERGED):
+                kname = abi.SCHEDULE_NAMES[sched]   # k_step_tri / k_step_merged
             traffic = None
             if os.path.exists(args.traffic):
                 try:

@@ -216,6 +216,10 @@ int xrt_test_trig_draw_domain(xrt_ctx* ctx, uint32_t first_bits, uint32_t count,
                               float* out_cos, float* out_r);
 /* glibc-logf/expf restatement on device over x[i]: out[2i] = logf, out[2i+1] = expf */
 int xrt_test_logexp(xrt_ctx* ctx, const float* x, uint32_t n, float* out);
+/* every 32-bit input: mode 0 checks the device's fast correctly rounded reciprocal against
+ * 1.0f / b, mode 1 its division by the constant c (rc = 1.0f / c) against x / c; returns the
+ * mismatch count and up to 16 mismatching inputs (0xffffffff = unused) */
+int xrt_test_fastdiv(xrt_ctx* ctx, uint32_t mode, float c, float rc, uint64_t* n_bad, uint32_t* first_bad16);
 
 #ifdef __cplusplus
 }

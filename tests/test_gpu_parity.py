@@ -150,6 +150,21 @@ def test_expf_restatement_negative_range(gpu):
     assert bad == 0
 
 
+@pytest.mark.parametrize("mode,c", [(0, 0.0), (1, "bsdf_pdf"), (1, 3.0)])
+def test_fast_division_is_ieee_on_every_float(gpu, mode, c):
+    """The kernels' fast reciprocal (Moller-Trumbore 1/det, orthonormalBasis) and divisions
+    by constants (Lambert pdf 1/(2*PI), Russian roulette /3) equal IEEE division on all 2^32
+    inputs (device_math.h rcp_rn / div_const)."""
+    if c == "bsdf_pdf":
+        c = np.float32(1.0) / (np.float32(2.0) * np.float32(3.14159265359))   # Src/material.h pdf
+    c = np.float32(c)
+    rc = np.float32(1.0) / c if mode == 1 else np.float32(0.0)
+    n = C.c_uint64(0)
+    bad = np.zeros(16, np.uint32)
+    assert abi.lib().xrt_test_fastdiv(gpu, mode, C.c_float(c), C.c_float(rc), C.byref(n), abi.u32ptr(bad)) == 0
+    assert n.value == 0, [hex(int(b)) for b in bad if b != 0xFFFFFFFF]
+
+
 # ------------------------------------------------------------------ images ----
 def test_c1_cornell_gi_bit_exact(renderer, sched):
     """Config C1 (Cornell 256x256x16, GIIntegrator(3)) — full framebuffer vs oracle."""

@@ -112,6 +112,7 @@ SIGNATURES = {
     "xrt_test_trig": (C.c_int, [C.c_void_p, f32p, C.c_uint32, f32p]),
     "xrt_test_trig_draw_domain": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, f32p, f32p, f32p]),
     "xrt_test_logexp": (C.c_int, [C.c_void_p, f32p, C.c_uint32, f32p]),
+    "xrt_test_fastdiv": (C.c_int, [C.c_void_p, C.c_uint32, C.c_float, C.c_float, C.POINTER(C.c_uint64), u32p]),
 }
 
 _lib = None

@@ -45,10 +45,40 @@ __device__ __forceinline__ float smax(float a, float b) { return (a < b) ? b : a
 __device__ __forceinline__ float comp(v3 a, uint32_t i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
 __device__ __forceinline__ v3 ray_at(v3 o, v3 d, float t) { return o + d * t; }   // Src/ray.h:20
 
+// ---- correctly rounded reciprocal / division by a constant, without v_div_* -----------
+// IEEE `1.0f / b` compiles to a ~10-instruction div_scale / rcp / 4 fma / div_fmas /
+// div_fixup sequence.  For b in the normal range, one Newton step on v_rcp_f32 already
+// gives the correctly rounded reciprocal, and Markstein's correction step turns q = x * rc
+// (rc = RN(1/c)) into RN(x / c).  Both are checked bit for bit against IEEE division on
+// every float input by tests/test_gpu_parity.py (xrt_test_fastdiv); inputs outside the
+// checked exponent window take the IEEE division.
+template <uint32_t LO, uint32_t HI>
+__device__ __forceinline__ bool fd_exp_in(float x) {   // biased exponent in [LO, HI]
+    const uint32_t e = (__float_as_uint(x) >> 23) & 0xffu;
+    return e - LO <= HI - LO;
+}
+__device__ __forceinline__ bool fd_normal(float x) { return fd_exp_in<2, 252>(x); }
+__device__ __forceinline__ float rcp_newton(float b) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
+}
+__device__ __forceinline__ float rcp_rn(float b) {   // == 1.0f / b
+    return fd_normal(b) ? rcp_newton(b) : 1.0f / b;
+}
+__device__ __forceinline__ float div_const_fast(float x, float c, float rc) {
+    const float q = x * rc;
+    return __builtin_fmaf(__builtin_fmaf(-c, q, x), rc, q);
+}
+// x / c for a constant c with rc = RN(1/c) (both normal): == x / c.  The residual
+// x - c*q is ~2^-24 x, so x's exponent must be >= 25 for it to stay a normal number.
+__device__ __forceinline__ float div_const(float x, float c, float rc) {
+    return fd_exp_in<25, 248>(x) ? div_const_fast(x, c, rc) : x / c;   // 248: |x / c| < 2^128 for c > 2^-4
+}
+
 // orthonormalBasis, active branch (Src/geometry.cpp:43-49)
 __device__ __forceinline__ void onb(v3 n, v3& t, v3& b) {
     const float sign = __builtin_copysignf(1.0f, n.z);
-    const float a = -1.0f / (sign + n.z);
+    const float a = -rcp_rn(sign + n.z);   // == -1.0f / (sign + n.z)
     const float c = n.x * n.y * a;
     t = mk(1.0f + sign * n.x * n.x * a, sign * c, -sign * n.x);
     b = mk(c, sign + n.y * n.y * a, -n.y);

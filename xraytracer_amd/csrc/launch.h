@@ -31,16 +31,18 @@ hipError_t launch_step(const KParams& P, const KParams* dP, const uint32_t* list
 // counter contract as launch_step)
 bool use_step_merged(const KParams& P);
 uint32_t step_merged_draws(const KParams& P);
-uint32_t step_merged_spw(const KParams& P);   // path slots per wave of the merged kernel
+uint32_t step_merged_spw(const KParams& P, uint64_t live);   // slots per wave for `live` live slots
 size_t step_merged_lds_bytes(const KParams& P);
 void build_step_objs(const DObjBox* boxes, int n, StepObjs& SO);
 hipError_t launch_step_merged(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                               const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
-                              uint32_t* req_count, uint32_t visits, uint32_t blocks, hipStream_t st);
+                              uint32_t* req_count, uint32_t visits, uint64_t live, hipStream_t st);
 hipError_t launch_finish(const KParams& P, hipStream_t st);
 hipError_t launch_test_rng(const uint32_t* seeds, uint32_t n_seeds, uint32_t skip, uint32_t n, float* out,
                            uint32_t* rings, hipStream_t st);
 hipError_t launch_test_trig(const float* x, uint32_t n, float* out, hipStream_t st);
 hipError_t launch_test_trig_domain(uint32_t first, uint32_t count, float* s, float* c, float* r, hipStream_t st);
 hipError_t launch_test_logexp(const float* x, uint32_t n, float* out, hipStream_t st);
+hipError_t launch_test_fastdiv(uint32_t mode, float c, float rc, uint32_t first, uint32_t count,
+                               unsigned long long* nbad, uint32_t* bad, hipStream_t st);
 }  // namespace xrt

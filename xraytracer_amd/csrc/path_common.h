@@ -157,7 +157,7 @@ __device__ __forceinline__ bool ray_tri(v3 o, v3 d, v3 v0, v3 e1, v3 e2, float& 
     const v3 pvec = cross(d, e2);
     const float det = dot(e1, pvec);
     if (__builtin_fabsf(det) < kEPSILON) return false;
-    const float invDet = 1.0f / det;
+    const float invDet = rcp_rn(det);   // == 1.0f / det
     const v3 tvec = o - v0;
     u = dot(tvec, pvec) * invDet;
     if (u < 0.0f || u > 1.0f) return false;

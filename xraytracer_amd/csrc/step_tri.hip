@@ -46,6 +46,10 @@ __device__ __forceinline__ v3 ld3g(const f4* p, size_t i) {
     return mk(q[0], q[1], q[2]);
 }
 
+constexpr float kRcp3 = 1.0f / 3.0f;                         // RN(1/3) for div_const
+constexpr float kLambertPdf = 1.0f / (2.0f * kPI);            // Lambert sampleBxDF pdf
+constexpr float kLambertPdfRcp = 1.0f / kLambertPdf;          // RN(1/pdf)
+
 // Stream words of one slot held in registers: b[0] is the next draw.  A segment draws at
 // most NW words (checked before it starts), so there is no fallback load.
 template <int NW>
@@ -99,7 +103,7 @@ __device__ __forceinline__ bool obj_overlap(v3 o, v3 inv, const StepObj& B, floa
 __device__ __forceinline__ bool ray_tri_nb(v3 o, v3 d, v3 v0, v3 e1, v3 e2, float& t) {
     const v3 pvec = cross(d, e2);
     const float det = dot(e1, pvec);
-    const float invDet = 1.0f / det;
+    const float invDet = rcp_rn(det);   // == 1.0f / det
     const v3 tvec = o - v0;
     const float u = dot(tvec, pvec) * invDet;
     const v3 qvec = cross(tvec, e1);
@@ -290,7 +294,7 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, int lan
 // (redundantly, results identical) and the group shares the traces (group_trace).  Either
 // way, with few slots per GPU (a pixel shard of a multi-GPU frame) this puts more, shorter
 // waves on every SIMD.
-template <int INTEG, int NL, int SPW, int G>
+template <int INTEG, int NL, int SPW, int G, bool LANE>
 __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
     const KParams* __restrict__ Pp, const StepObjs SO, const uint32_t* __restrict__ list,
     const uint32_t* __restrict__ count, uint32_t* __restrict__ out, uint32_t* out_count, uint32_t* zero_count,
@@ -317,7 +321,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
     lds_copy(const_cast<f4*>(L.nrm), P.tri_nrm, 3 * P.n_tris, tid);
     lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
     lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid);
-    if (G > 1) lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid);
+    if (LANE) lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid);
     __syncthreads();
 #ifdef XRT_PHASE_CLOCK
     uint64_t ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -424,7 +428,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
             MPH_MARK(0);
             unsigned long long best;
             uint32_t occ;
-            if constexpr (G == 1)
+            if constexpr (!LANE)
                 merged_trace<NL>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ PH_TARGS);
             else
                 group_trace<NL, G>(P.n_objs, L, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
@@ -463,7 +467,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                     } else {
                         alive = true;
                         if (depth > 0) {
-                            const float pr = smin((thr.x + thr.y + thr.z) / 3.0f, 1.0f);
+                            const float pr = smin(div_const(thr.x + thr.y + thr.z, 3.0f, kRcp3), 1.0f);
                             if (rng.next() >= pr) alive = false, ended = true;
                             else thr = thr / mk(pr, pr, pr);
                         }
@@ -489,14 +493,17 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                             shm |= 1u << l;
                             const float bias = 0.01f;
                             so[l] = pos + ng * bias, sd[l] = wi, stm[l] = tmax - bias;
-                            if constexpr (G == 1) {
+                            if constexpr (!LANE) {
                                 W.ro[(1 + l) * 64 + lane] = make_float4(so[l].x, so[l].y, so[l].z, stm[l]);
                                 W.rd[(1 + l) * 64 + lane] = make_float4(wi.x, wi.y, wi.z, 0.0f);
                             }
                             const float cosv = smax(0.0f, dot(ng, wi));
-                            // vis * fr * L * cos / pdf (Src/integrator.h:250-262) for vis = 1, 0
-                            c1[l] = (((fr * 1.0f) * Lv) * cosv) / pdf;
-                            c0[l] = (((fr * 0.0f) * Lv) * cosv) / pdf;
+                            // vis * fr * L * cos / pdf (Src/integrator.h:250-262) for vis = 1, 0.
+                            // fr * 1 == fr; for vis = 0 the product is +-0 or NaN and pdf is
+                            // > 0 (or NaN), so the quotient is that product (NaN for a NaN pdf)
+                            c1[l] = ((fr * Lv) * cosv) / pdf;
+                            const v3 z = ((fr * 0.0f) * Lv) * cosv;
+                            c0[l] = pdf == pdf ? z : mk(pdf, pdf, pdf);
                         }
                     }
                     if (INTEG == XRT_INTEGRATOR_DIRECT) {
@@ -504,16 +511,20 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                     } else {
                         if (shm) thr_nee = thr;
                         else rad = rad + thr * mk(0.0f, 0.0f, 0.0f);   // no shadow ray: directL = 0
-                        float pdf = 1.0f;
                         v3 nd = mk(0, 0, 0);
-                        if (ob.material == 1) {
+                        const bool lamb = ob.material == 1;
+                        if (lamb) {
                             v3 dpdu, dpdv;
                             onb(tri_ns_l(L, hk, hu, hv), dpdu, dpdv);
                             nd = lambert_sample_f(ng, dpdu, dpdv, rng);
-                            pdf = 1.0f / (2.0f * kPI);
                         }
                         const float cosv = smax(0.0f, dot(nd, ng));
-                        thr = thr * ((fr * cosv) / pdf);
+                        // (fr * cos) / pdf, pdf = 1 / (2 PI) for Lambert (Src/material.h:60-73), else 1
+                        const v3 fc = fr * cosv;
+                        thr = thr * (lamb ? mk(div_const(fc.x, kLambertPdf, kLambertPdfRcp),
+                                               div_const(fc.y, kLambertPdf, kLambertPdfRcp),
+                                               div_const(fc.z, kLambertPdf, kLambertPdfRcp))
+                                          : fc / 1.0f);
                         o = pos + ng * 0.01f;
                         d = nd;
                         ++depth;
@@ -542,7 +553,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
         if (__ballot(shm != 0)) {
             unsigned long long best;
             uint32_t occ;
-            if constexpr (G == 1)
+            if constexpr (!LANE)
                 merged_trace<NL>(SO, L, W, lane, false, o, d, shm, so, sd, stm, best, occ PH_TARGS);
             else
                 group_trace<NL, G>(P.n_objs, L, lane, false, o, d, shm, so, sd, stm, best, occ);
@@ -618,14 +629,14 @@ void build_step_objs(const DObjBox* boxes, int n, StepObjs& SO) {
     }
 }
 
-template <int INTEG, int SPW, int G>
+template <int INTEG, int SPW, int G, bool LANE>
 static void launch_merged_i(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                             const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
                             uint32_t* req_count, uint32_t visits, size_t lds, hipStream_t st) {
     const uint32_t per_block = (kBlock / 64) * SPW;
     const uint32_t blocks = P.n_part * ((P.part_cap + per_block - 1) / per_block);
 #define XRT_LAUNCH_MERGED(NLV)                                                                                       \
-    hipLaunchKernelGGL((k_step_merged<INTEG, NLV, SPW, G>), dim3(blocks), dim3(kBlock), lds, st, dP, SO, list, count, \
+    hipLaunchKernelGGL((k_step_merged<INTEG, NLV, SPW, G, LANE>), dim3(blocks), dim3(kBlock), lds, st, dP, SO, list, count, \
                        out, out_count, zero, req_count, visits)
     switch (P.n_lights) {
         case 0: XRT_LAUNCH_MERGED(0); break;
@@ -639,42 +650,42 @@ static void launch_merged_i(const KParams& P, const KParams* dP, const StepObjs&
 
 // slots per wave: as many as keep >= kMergedWavesWanted waves in flight for this shard
 // (XRT_MERGED_SPW overrides, for experiments; results do not depend on it)
-uint32_t step_merged_spw(const KParams& P) {
+uint32_t step_merged_spw(const KParams& P, uint64_t live) {
     if (const char* e = std::getenv("XRT_MERGED_SPW")) {
         const int v = std::atoi(e);
         if (v == 16 || v == 32 || v == 64) return (uint32_t)v;
     }
-    if (P.n_slots >= 64u * kMergedWavesWanted) return 64;
-    if (P.n_slots >= 32u * kMergedWavesWanted) return 32;
+    if (live >= 64ull * kMergedWavesWanted) return 64;
+    if (live >= 32ull * kMergedWavesWanted) return 32;
     return 16;
 }
 
 template <int INTEG>
 static void launch_merged_spw(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                               const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
-                              uint32_t* req_count, uint32_t visits, size_t lds, hipStream_t st) {
+                              uint32_t* req_count, uint32_t visits, uint64_t live, size_t lds, hipStream_t st) {
     const bool group = P.n_tris <= 64 && !std::getenv("XRT_NO_GROUP");   // group trace: 64-bit triangle masks
-#define XRT_MERGED_CASE(SPWV, GV) \
-    launch_merged_i<INTEG, SPWV, GV>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, lds, st)
-    switch (step_merged_spw(P)) {
-        case 64: XRT_MERGED_CASE(64, 1); break;
-        case 32: if (group) XRT_MERGED_CASE(32, 2); else XRT_MERGED_CASE(32, 1); break;
-        default: if (group) XRT_MERGED_CASE(16, 4); else XRT_MERGED_CASE(16, 1); break;
+    const bool lane64 = group && std::getenv("XRT_LANE_TRACE");   // experiment: per-lane traces, full waves
+#define XRT_MERGED_CASE(SPWV, GV, LV) \
+    launch_merged_i<INTEG, SPWV, GV, LV>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, lds, st)
+    switch (step_merged_spw(P, live)) {
+        case 64: if (lane64) XRT_MERGED_CASE(64, 1, true); else XRT_MERGED_CASE(64, 1, false); break;
+        case 32: if (group) XRT_MERGED_CASE(32, 2, true); else XRT_MERGED_CASE(32, 1, false); break;
+        default: if (group) XRT_MERGED_CASE(16, 4, true); else XRT_MERGED_CASE(16, 1, false); break;
     }
 #undef XRT_MERGED_CASE
 }
 
 hipError_t launch_step_merged(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                               const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
-                              uint32_t* req_count, uint32_t visits, uint32_t blocks, hipStream_t st) {
-    (void)blocks;   // the grid follows the slots-per-wave choice
+                              uint32_t* req_count, uint32_t visits, uint64_t live, hipStream_t st) {
     const size_t lds = step_merged_lds_bytes(P);
     if (P.integrator == XRT_INTEGRATOR_DIRECT)
         launch_merged_spw<XRT_INTEGRATOR_DIRECT>(P, dP, SO, list, count, out, out_count, zero, req_count, visits,
-                                                 lds, st);
+                                                 live, lds, st);
     else
-        launch_merged_spw<XRT_INTEGRATOR_GI>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, lds,
-                                             st);
+        launch_merged_spw<XRT_INTEGRATOR_GI>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, live,
+                                             lds, st);
     return hipGetLastError();
 }
 

@@ -30,7 +30,8 @@ constexpr uint32_t kRngVisit = 16;   // a slot visit needs at least this many (m
 constexpr uint32_t kMaxParts = 64;   // live-list partitions (counters per list)
 constexpr uint32_t kRefillEvery = 4; // wavefront schedule: k_refill after every 4th k_shade
 constexpr uint32_t kStepVisits = 32; // fused schedule: path segments per slot per k_step
-constexpr uint32_t kMergedVisits = 32; // merged-trace schedule: segments per slot per launch
+constexpr uint32_t kMergedVisits = 64; // merged-trace schedule: segments per slot per launch (at most;
+                                       // clamped so a launch's draws fit one refill block)
 constexpr uint32_t kMergedWavesWanted = 2048; // merged-trace schedule: waves to keep in flight (2 per SIMD)
 constexpr uint32_t kStepRefill = 1;  // fused schedule: k_refill after every k_step
 constexpr uint32_t kVisitDraws = 13; // max RNG draws of one GI/Direct segment (4 lights)

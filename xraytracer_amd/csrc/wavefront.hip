@@ -1638,6 +1638,29 @@ __global__ void k_test_trig_domain(uint32_t first, uint32_t count, float* out_si
     out_cos[i] = glibc_cosf(phi);
 }
 
+// fast-division self-test over every 32-bit pattern in [first, first + count): mode 0 checks
+// rcp_rn(b) against 1.0f / b; mode 1 checks div_const(x, c, rc) against x / c.  Counts
+// mismatches (NaN == NaN) and records the first 16.
+__global__ void k_test_fastdiv(uint32_t mode, float c, float rc, uint32_t first, uint32_t count,
+                               unsigned long long* nbad, uint32_t* bad) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const float x = __uint_as_float(first + i);
+    float f, r;
+    if (mode == 0) {
+        f = rcp_rn(x);
+        r = 1.0f / x;
+    } else {
+        f = div_const(x, c, rc);
+        r = x / c;
+    }
+    const bool same = __float_as_uint(f) == __float_as_uint(r) || (f != f && r != r);
+    if (!same) {
+        const unsigned long long k = atomicAdd(nbad, 1ull);
+        if (k < 16) bad[k] = first + i;
+    }
+}
+
 __global__ void k_test_logexp(const float* x, uint32_t n, float* out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
@@ -1790,6 +1813,13 @@ hipError_t launch_test_trig(const float* x, uint32_t n, float* out, hipStream_t 
 
 hipError_t launch_test_trig_domain(uint32_t first, uint32_t count, float* s, float* c, float* r, hipStream_t st) {
     hipLaunchKernelGGL(k_test_trig_domain, dim3((count + 255) / 256), dim3(256), 0, st, first, count, s, c, r);
+    return hipGetLastError();
+}
+
+hipError_t launch_test_fastdiv(uint32_t mode, float c, float rc, uint32_t first, uint32_t count,
+                               unsigned long long* nbad, uint32_t* bad, hipStream_t st) {
+    hipLaunchKernelGGL(k_test_fastdiv, dim3((count + 255) / 256), dim3(256), 0, st, mode, c, rc, first, count, nbad,
+                       bad);
     return hipGetLastError();
 }
 

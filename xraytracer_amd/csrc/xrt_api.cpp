@@ -471,7 +471,9 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     const bool merged = fused && !(p->flags & XRT_FLAG_NO_MERGED) && use_step_merged(P);
     // tuning knobs (defaults kStepVisits / kStepRefill; XRT_STEP_VISITS / XRT_STEP_REFILL
     // override them for experiments — results do not depend on them)
-    const uint32_t step_visits = env_u32("XRT_STEP_VISITS", merged ? kMergedVisits : kStepVisits, 1, 128);
+    const uint32_t merged_visits =
+        merged ? std::min<uint32_t>(kMergedVisits, (kMT - step_merged_draws(P)) / step_merged_draws(P)) : 0;
+    const uint32_t step_visits = env_u32("XRT_STEP_VISITS", merged ? merged_visits : kStepVisits, 1, 128);
     const uint32_t step_refill = env_u32("XRT_STEP_REFILL", kStepRefill, 1, 8);
     // a slot queues a refill when fewer words are left than the next `refill` launches can
     // draw: the merged kernel draws at most step_merged_draws per segment and checks it
@@ -482,18 +484,25 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     if ((rc = ensure(c, c->kparams, sizeof(KParams)))) return rc;
     HIPCHK(c, hipMemcpyAsync(c->kparams.p, &P, sizeof(KParams), hipMemcpyHostToDevice, c->stream));
     const KParams* dP = as<KParams>(c->kparams);
-    const uint64_t poll_every = fused ? 4 : kPoll, ahead = fused ? 16 : kAhead;
+    const uint64_t poll_every = merged ? 1 : fused ? 4 : kPoll, ahead = merged ? 4 : fused ? 16 : kAhead;
+    // merged schedule: the slots-per-wave layout of each launch follows the latest polled
+    // live-slot count (full waves while the frame is busy, 2 or 4 lanes per slot for the
+    // long-chain pixels left at its end); every layout gives identical results
+    uint64_t live_hint = n;
+    std::vector<uint64_t> launch_live;   // the live hint each step launch was sized with
+    size_t step_idx = 0;
     for (; it < cap_iters && !done; ++it) {
         const int cur = (int)(it & 1), nxt = cur ^ 1;
         uint32_t* live = nullptr;
         if (fused) {
             const int ci = (int)(it % 3), co = (int)((it + 1) % 3), cz = (int)((it + 2) % 3);
             live = counts_at(co);
+            launch_live.push_back(live_hint);
             hipError_t e = launch(XRT_K_STEP, [&] {
                 if (merged)
                     return launch_step_merged(P, dP, c->step_objs, lists[cur], counts_at(ci), lists[nxt],
                                               counts_at(co), counts_at(cz), req_counts + (epoch & 1) * kMaxParts,
-                                              step_visits, blocks, c->stream);
+                                              step_visits, live_hint, c->stream);
                 return launch_step(P, dP, lists[cur], counts_at(ci), lists[nxt], counts_at(co), counts_at(cz),
                                    req_counts + (epoch & 1) * kMaxParts, step_visits, blocks, c->stream);
             });
@@ -533,6 +542,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             HIPCHK(c, hipEventSynchronize(q.ev));
             uint64_t alive = 0;
             for (uint32_t k = 0; k < P.n_part; ++k) alive += c->h_poll[q.slot * kMaxParts + k];
+            live_hint = alive;
             if (alive == 0) done = true;
             polls.erase(polls.begin());
             if (done) break;
@@ -566,10 +576,23 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
                  : merged ? XRT_SCHED_STEP_MERGED
                  : use_step_tri(P) ? XRT_SCHED_STEP_TRI : XRT_SCHED_STEP;
     if (timing) {
-        for (auto& u : ev_use) {
+        const bool trace = std::getenv("XRT_TRACE_LAUNCHES") != nullptr;   // experiments: per-launch times
+        for (size_t q = 0; q < ev_use.size(); ++q) {
+            const auto& u = ev_use[q];
             float ms = 0.0f;
             if (hipEventElapsedTime(&ms, c->events[u.second], c->events[u.second + 1]) == hipSuccess)
                 S.kernel_ms[u.first] += ms;
+            if (trace) {
+                float gap = 0.0f;
+                if (q) (void)hipEventElapsedTime(&gap, c->events[ev_use[q - 1].second + 1], c->events[u.second]);
+                std::fprintf(stderr, "[xrt] launch %zu kernel %d %.3f ms (gap %.3f)%s", q, u.first, ms, gap,
+                             u.first == XRT_K_STEP && q < launch_live.size() + 2 ? "" : "\n");
+                if (u.first == XRT_K_STEP) {
+                    const size_t si = step_idx++;
+                    std::fprintf(stderr, " live %llu\n",
+                                 si < launch_live.size() ? (unsigned long long)launch_live[si] : 0ull);
+                }
+            }
         }
     }
     if (h_out) HIPCHK(c, hipMemcpy(h_out, fb, npix * 3 * sizeof(float), hipMemcpyDeviceToHost));
@@ -650,3 +673,24 @@ int xrt_test_trig_draw_domain(xrt_ctx* c, uint32_t first, uint32_t count, float*
 }
 
 }  // extern "C"
+
+// every 32-bit input: mode 0 rcp_rn vs 1/b, mode 1 div_const(x, c, rc) vs x / c (device_math.h)
+int xrt_test_fastdiv(xrt_ctx* c, uint32_t mode, float cst, float rc, uint64_t* n_bad, uint32_t* first_bad16) {
+    if (!c || !n_bad || !first_bad16) return XRT_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    unsigned long long* d_n = nullptr;
+    uint32_t* d_bad = nullptr;
+    HIPCHK(c, hipMalloc(&d_n, 8));
+    HIPCHK(c, hipMalloc(&d_bad, 64));
+    hipError_t e = hipMemsetAsync(d_n, 0, 8, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d_bad, 0xff, 64, c->stream);
+    const uint32_t chunk = 1u << 30;
+    for (uint64_t f = 0; f < (1ull << 32) && e == hipSuccess; f += chunk)
+        e = launch_test_fastdiv(mode, cst, rc, (uint32_t)f, chunk, d_n, d_bad, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(n_bad, d_n, 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(first_bad16, d_bad, 64, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d_n);
+    (void)hipFree(d_bad);
+    return e == hipSuccess ? XRT_OK : hip_err(c, e, "xrt_test_fastdiv");
+}
