@@ -37,6 +37,8 @@ void build_step_objs(const DObjBox* boxes, int n, StepObjs& SO);
 hipError_t launch_step_merged(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                               const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
                               uint32_t* req_count, uint32_t visits, uint64_t live, hipStream_t st);
+// the merged schedule's refill (leaves ST_RNGREQ to the merged kernel; see step_tri.hip)
+hipError_t launch_refill_merged(const KParams& P, const uint32_t* count, uint32_t* zero_count, hipStream_t st);
 hipError_t launch_finish(const KParams& P, hipStream_t st);
 hipError_t launch_test_rng(const uint32_t* seeds, uint32_t n_seeds, uint32_t skip, uint32_t n, float* out,
                            uint32_t* rings, hipStream_t st);

@@ -337,6 +337,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
         const bool lead = own && (lane % G) == 0;   // the lane of a group that writes back
         const uint32_t s = own ? list[it.p * P.part_cap + i] : 0;
         uint32_t st = own ? glb<gu32>(P.state)[s] : ST_DONE;
+        st &= ~ST_RNGREQ;   // the refill this slot asked for ran after the previous launch
         const bool live = !(st & ST_DONE);
         uint32_t g = 0, depth = 0, k = 0, kst = 0;   // k: finished samples, kst: started samples
         RngRegs<NW> rng;
@@ -594,6 +595,75 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
 #endif
 }
 
+// --------------------------------------------------------------- RNG refills ----
+// k_refill_merged: the merged schedule's ring refill.  Same twist as wave_twist (libstdc++
+// _M_gen_rand: x[g+k] = x[g+k-227] ^ mix(x[g+k-624], x[g+k-623]), chunks k = m, 227+m,
+// 454+m held in registers), arranged for bandwidth: every load of a twist is issued before
+// the first use (clamped indices instead of guarded loads), the next request's slot and
+// stream position are fetched while the current one twists, and the slot state is not
+// touched — the merged kernel clears ST_RNGREQ when it next loads the slot, which is always
+// after this kernel (one refill launch follows every step launch).
+__device__ __forceinline__ void twist_block(uint32_t* ring, uint32_t g, int lane) {
+    const uint32_t h = g % kRing;
+    gu32* old = glb<gu32>(ring + (kMT - h));
+    uint32_t* nw = ring + h;
+    uint32_t x0[4], x1[4], x397[4], y0[4], y1[4], z0[3], z1[3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t m = min((uint32_t)lane + 64u * j, 226u);
+        x0[j] = old[m], x1[j] = old[m + 1], x397[j] = old[m + 397];
+        y0[j] = old[227 + m], y1[j] = old[228 + m];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const uint32_t m = min((uint32_t)lane + 64u * j, 169u);
+        z0[j] = old[454 + m], z1[j] = old[min(455 + m, kMT - 1)];
+    }
+    uint32_t a[4], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = x397[j] ^ mt_mix(x0[j], x1[j]);
+    const uint32_t n0 = __builtin_amdgcn_readfirstlane(a[0]);   // x[g]: the new block's first word
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = a[j] ^ mt_mix(y0[j], y1[j]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const uint32_t m = (uint32_t)lane + 64u * j;
+        if (m < 170u) nw[454 + m] = b[j] ^ mt_mix(z0[j], m + 455 < kMT ? z1[j] : n0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t m = (uint32_t)lane + 64u * j;
+        if (m < 227u) nw[m] = a[j], nw[227 + m] = b[j];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_refill_merged(KParams P, const uint32_t* __restrict__ req,
+                                                          const uint32_t* __restrict__ count, uint32_t* zero_count) {
+    zero_parts(P, zero_count);
+    const PartIter it = part_iter(P, count, kBlock / 64);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t i = it.first + wv;
+    if (i >= it.n) return;
+    const uint32_t* rq = req + it.p * P.part_cap;
+    uint32_t s = rq[i];
+    uint32_t g = glb<gu32>(P.rng_g)[s];
+    while (true) {
+        const uint32_t in = i + it.stride;
+        const uint32_t sn = in < it.n ? rq[in] : s;
+        twist_block(P.ring + (size_t)s * kRing, g, lane);
+        if (lane == 0) P.rng_g[s] = g + kMT;
+        if (in >= it.n) break;
+        g = glb<gu32>(P.rng_g)[sn];
+        s = sn, i = in;
+    }
+}
+
+hipError_t launch_refill_merged(const KParams& P, const uint32_t* count, uint32_t* zero_count, hipStream_t st) {
+    const uint32_t per = std::max<uint32_t>(1u, std::min<uint32_t>((P.part_cap + 3) / 4, 4096u / P.n_part));
+    hipLaunchKernelGGL(k_refill_merged, dim3(P.n_part * per), dim3(kBlock), 0, st, P, P.req, count, zero_count);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------- host side ----
 bool use_step_merged(const KParams& P) {
     return P.scene_kind == SCN_TRI && P.small_tri && P.n_objs <= kMergedMaxObjs && P.n_lights <= kMaxLights &&
@@ -648,15 +718,17 @@ static void launch_merged_i(const KParams& P, const KParams* dP, const StepObjs&
 #undef XRT_LAUNCH_MERGED
 }
 
-// slots per wave: as many as keep >= kMergedWavesWanted waves in flight for this shard
+// slots per wave for a shard of `live` slots
 // (XRT_MERGED_SPW overrides, for experiments; results do not depend on it)
 uint32_t step_merged_spw(const KParams& P, uint64_t live) {
     if (const char* e = std::getenv("XRT_MERGED_SPW")) {
         const int v = std::atoi(e);
         if (v == 16 || v == 32 || v == 64) return (uint32_t)v;
     }
-    if (live >= 64ull * kMergedWavesWanted) return 64;
-    if (live >= 32ull * kMergedWavesWanted) return 32;
+    // measured on C2 (tools/shard_sim.py): full waves down to ~160k live
+    // slots, 32 slots per wave down to ~90k, then 16 (4 lanes per slot)
+    if (live >= kMergedLive64) return 64;
+    if (live >= kMergedLive32) return 32;
     return 16;
 }
 

@@ -32,7 +32,8 @@ constexpr uint32_t kRefillEvery = 4; // wavefront schedule: k_refill after every
 constexpr uint32_t kStepVisits = 32; // fused schedule: path segments per slot per k_step
 constexpr uint32_t kMergedVisits = 64; // merged-trace schedule: segments per slot per launch (at most;
                                        // clamped so a launch's draws fit one refill block)
-constexpr uint32_t kMergedWavesWanted = 2048; // merged-trace schedule: waves to keep in flight (2 per SIMD)
+constexpr uint32_t kMergedLive64 = 160000;  // merged-trace schedule: live slots for 64 slots per wave
+constexpr uint32_t kMergedLive32 = 90000;   // ... and for 32 (below: 16 slots, 4 lanes each)
 constexpr uint32_t kStepRefill = 1;  // fused schedule: k_refill after every k_step
 constexpr uint32_t kVisitDraws = 13; // max RNG draws of one GI/Direct segment (4 lights)
 // fused schedule: a slot queues a refill when fewer than refill * visits * 13 + kRngVisit

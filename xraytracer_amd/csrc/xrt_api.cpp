@@ -433,10 +433,13 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     // consumes it and clears req_counts[(e + 1) & 1] for epoch e + 1.  Epoch 0 is the
     // first twist of every slot, requested by k_seed.
     uint64_t epoch = 0;
+    bool merged_refill = false;   // set once the merged schedule is chosen (below)
     auto refill = [&]() -> hipError_t {
         const int a = (int)(epoch & 1), b = a ^ 1;
         ++epoch;
         return launch(XRT_K_REFILL, [&] {
+            if (merged_refill)
+                return launch_refill_merged(P, req_counts + a * kMaxParts, req_counts + b * kMaxParts, c->stream);
             return launch_refill(P, req_counts + a * kMaxParts, req_counts + b * kMaxParts, c->stream);
         });
     };
@@ -474,7 +477,10 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     const uint32_t merged_visits =
         merged ? std::min<uint32_t>(kMergedVisits, (kMT - step_merged_draws(P)) / step_merged_draws(P)) : 0;
     const uint32_t step_visits = env_u32("XRT_STEP_VISITS", merged ? merged_visits : kStepVisits, 1, 128);
-    const uint32_t step_refill = env_u32("XRT_STEP_REFILL", kStepRefill, 1, 8);
+    // the merged kernel relies on one refill launch after every step launch (it clears
+    // ST_RNGREQ itself), so XRT_STEP_REFILL does not apply to it
+    const uint32_t step_refill = merged ? 1u : env_u32("XRT_STEP_REFILL", kStepRefill, 1, 8);
+    merged_refill = merged;
     // a slot queues a refill when fewer words are left than the next `refill` launches can
     // draw: the merged kernel draws at most step_merged_draws per segment and checks it
     P.rng_keep = merged ? step_refill * step_visits * step_merged_draws(P) + step_merged_draws(P)
@@ -484,11 +490,12 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     if ((rc = ensure(c, c->kparams, sizeof(KParams)))) return rc;
     HIPCHK(c, hipMemcpyAsync(c->kparams.p, &P, sizeof(KParams), hipMemcpyHostToDevice, c->stream));
     const KParams* dP = as<KParams>(c->kparams);
-    const uint64_t poll_every = merged ? 1 : fused ? 4 : kPoll, ahead = merged ? 4 : fused ? 16 : kAhead;
-    // merged schedule: the slots-per-wave layout of each launch follows the latest polled
-    // live-slot count (full waves while the frame is busy, 2 or 4 lanes per slot for the
-    // long-chain pixels left at its end); every layout gives identical results
-    uint64_t live_hint = n;
+    const uint64_t poll_every = merged ? 2 : fused ? 4 : kPoll, ahead = merged ? 6 : fused ? 16 : kAhead;
+    // merged schedule: the slots-per-wave layout is chosen from the shard's slot count (full
+    // waves for a whole frame, 2 or 4 lanes per slot for small pixel shards); switching it
+    // as the live count drops measured slower.  Every layout gives identical
+    // results.
+    const uint64_t live_hint = n;
     std::vector<uint64_t> launch_live;   // the live hint each step launch was sized with
     size_t step_idx = 0;
     for (; it < cap_iters && !done; ++it) {
@@ -542,7 +549,6 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             HIPCHK(c, hipEventSynchronize(q.ev));
             uint64_t alive = 0;
             for (uint32_t k = 0; k < P.n_part; ++k) alive += c->h_poll[q.slot * kMaxParts + k];
-            live_hint = alive;
             if (alive == 0) done = true;
             polls.erase(polls.begin());
             if (done) break;
