@@ -100,50 +100,58 @@ __device__ __forceinline__ v3 local_to_world(v3 v, v3 lx, v3 ly, v3 lz) {
 // c3, s3, c4).  tests/test_trig.py checks it bit-for-bit against the host libm over every
 // phi = 2*PI*r that the reference's sampler can produce (83,886,080 values) — identical
 // for both glibc build variants (with and without FMA contraction).
-struct SinCosTab {
-    double sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4;
-};
-static __constant__ const SinCosTab kSinCosTab[2] = {
-    {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, 0x1p0, -0x1.ffffffd0c621cp-2,
-     -0x1.555545995a603p-3, 0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10,
-     -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16},
-    {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, -0x1p0, 0x1.ffffffd0c621cp-2,
-     -0x1.555545995a603p-3, -0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10,
-     -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16}};
-__device__ __forceinline__ const SinCosTab& sincos_tab(int i) { return kSinCosTab[i]; }
+// The two coefficient sets of __sincosf_table differ only in the sign of every cosine
+// coefficient (c0..c4), and IEEE negation commutes exactly with * and +, so the second
+// set's cosine polynomial is the exact negation of the first's; the quadrant sign table is
+// {1, -1, -1, 1}.  Both are applied with selects, so no lane reads a table from memory (a
+// per-lane table index made every Lambert sample wait on a global load).
+constexpr double kSC_hpi_inv = 0x1.45f306dc9c883p+23, kSC_hpi = 0x1.921fb54442d18p+0;
+constexpr double kSC_c0 = 0x1p0, kSC_c1 = -0x1.ffffffd0c621cp-2, kSC_c2 = 0x1.55553e1068f19p-5,
+                 kSC_c3 = -0x1.6c087e89a359dp-10, kSC_c4 = 0x1.99343027bf8c3p-16;
+constexpr double kSC_s1 = -0x1.555545995a603p-3, kSC_s2 = 0x1.1107605230bc4p-7, kSC_s3 = -0x1.994eb3774cf24p-13;
 __device__ __forceinline__ uint32_t abstop12(float x) { return (__float_as_uint(x) >> 20) & 0x7ff; }
-__device__ __forceinline__ float sincosf_poly(double x, double x2, const SinCosTab& p, int n) {
-    if ((n & 1) == 0) {
-        const double x3 = x * x2;
-        const double s1 = p.s2 + x2 * p.s3;
-        const double x7 = x3 * x2;
-        const double s = x + x3 * p.s1;
-        return (float)(s + x7 * s1);
-    }
-    const double x4 = x2 * x2;
-    const double c2 = p.c3 + x2 * p.c4;
-    const double c1 = p.c0 + x2 * p.c1;
-    const double x6 = x4 * x2;
-    const double c = c1 + x4 * p.c2;
-    return (float)(c + x6 * c2);
+// sincosf_poly, sine branch (n even): x + x^3 s1 + x^7 (s2 + x^2 s3)
+__device__ __forceinline__ float sincosf_sin_poly(double x, double x2) {
+    const double x3 = x * x2;
+    const double s1 = kSC_s2 + x2 * kSC_s3;
+    const double x7 = x3 * x2;
+    const double s = x + x3 * kSC_s1;
+    return (float)(s + x7 * s1);
 }
-__device__ __forceinline__ double sincosf_reduce(double x, const SinCosTab& p, int& n) {
-    const double r = x * p.hpi_inv;
+// sincosf_poly, cosine branch (n odd) with the first coefficient set
+__device__ __forceinline__ double sincosf_cos_poly(double x2) {
+    const double x4 = x2 * x2;
+    const double c2 = kSC_c3 + x2 * kSC_c4;
+    const double c1 = kSC_c0 + x2 * kSC_c1;
+    const double x6 = x4 * x2;
+    const double c = c1 + x4 * kSC_c2;
+    return c + x6 * c2;
+}
+__device__ __forceinline__ double sincosf_reduce(double x, int& n) {
+    const double r = x * kSC_hpi_inv;
     n = (((int32_t)r) + 0x800000) >> 24;
-    return x - n * p.hpi;
+    return x - n * kSC_hpi;
+}
+// sincosf_poly(x * sign[n & 3], x * x, table (n & 2) ? 1 : 0, n) for quadrant n
+__device__ __forceinline__ float sincosf_quadrant(double x, int n) {
+    if ((n & 1) == 0) {
+        const double sg = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;   // sign[n & 3] (n even: 1 or -1)
+        return sincosf_sin_poly(x * sg, x * x);
+    }
+    const double c = sincosf_cos_poly(x * x);
+    return (float)((n & 2) ? -c : c);
 }
 __device__ __forceinline__ float glibc_sinf(float y) {
     const float pio4f = 0x1.921FB6p-1f;
     double x = y;
     if (abstop12(y) < abstop12(pio4f)) {
         if (abstop12(y) < abstop12(0x1p-12f)) return y;
-        return sincosf_poly(x, x * x, sincos_tab(0), 0);
+        return sincosf_sin_poly(x, x * x);
     }
     if (abstop12(y) < abstop12(120.0f)) {
         int n;
-        x = sincosf_reduce(x, sincos_tab(0), n);
-        const double s = sincos_tab(0).sign[n & 3];
-        return sincosf_poly(x * s, x * x, sincos_tab((n & 2) ? 1 : 0), n);
+        x = sincosf_reduce(x, n);
+        return sincosf_quadrant(x, n);
     }
     return __builtin_sinf(y);  // |x| >= 120: outside every domain this renderer samples
 }
@@ -152,13 +160,19 @@ __device__ __forceinline__ float glibc_cosf(float y) {
     double x = y;
     if (abstop12(y) < abstop12(pio4f)) {
         if (abstop12(y) < abstop12(0x1p-12f)) return 1.0f;
-        return sincosf_poly(x, x * x, sincos_tab(0), 1);
+        return (float)sincosf_cos_poly(x * x);
     }
     if (abstop12(y) < abstop12(120.0f)) {
         int n;
-        x = sincosf_reduce(x, sincos_tab(0), n);
-        const double s = sincos_tab(0).sign[n & 3];
-        return sincosf_poly(x * s, x * x, sincos_tab((n & 2) ? 1 : 0), n ^ 1);
+        x = sincosf_reduce(x, n);
+        // glibc: sincosf_poly(x * sign[n & 3], x * x, table (n & 2), n ^ 1): the sine branch
+        // takes the sign of quadrant n, the cosine branch the table of quadrant n
+        if (((n ^ 1) & 1) == 0) {
+            const double sg = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
+            return sincosf_sin_poly(x * sg, x * x);
+        }
+        const double c = sincosf_cos_poly(x * x);
+        return (float)((n & 2) ? -c : c);
     }
     return __builtin_cosf(y);
 }

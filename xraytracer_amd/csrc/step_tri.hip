@@ -324,7 +324,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
     if (LANE) lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid);
     __syncthreads();
 #ifdef XRT_PHASE_CLOCK
-    uint64_t ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t ph_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t ph_vis = 0, ph_cnt[3] = {0, 0, 0};
     const uint64_t kt0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -449,6 +449,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                 v3 pos = mk(0, 0, 0), ng = mk(0, 0, 0);
                 if (hk >= 0) pos = ray_at(o, d, ht), ng = xyz(L.tng[hk]);
                 bool ended = false, alive = false;
+                MPH_MARK(8);
                 if (INTEG == XRT_INTEGRATOR_DIRECT) {
                     // DirectIntegrator::integrate (Src/integrator.h:82-119)
                     if (obj < 0) {
@@ -479,6 +480,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                         }
                     }
                 }
+                MPH_MARK(9);
                 if (alive) {
                     // next-event estimation: light samples now, shadow rays traced with the
                     // next trace of the wave
@@ -507,6 +509,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                             c0[l] = pdf == pdf ? z : mk(pdf, pdf, pdf);
                         }
                     }
+                    MPH_MARK(10);
                     if (INTEG == XRT_INTEGRATOR_DIRECT) {
                         ended = true;
                     } else {
@@ -532,6 +535,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                         if (depth >= max_depth) ended = true;
                     }
                 }
+                MPH_MARK(11);
                 if (ended) {
                     ext = false;
                     if (shm) {
@@ -544,7 +548,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                 }
             }
             MPH_MARK(3);
-            if (act) rng.load(ring);
+            rng.load(ring);   // unconditional: the loads land straight in the loop-carried registers (no copy that would wait on them)
 #ifdef XRT_PHASE_CLOCK
             ++ph_vis;
 #endif
@@ -586,6 +590,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
 #ifdef XRT_PHASE_CLOCK
     if (lane == 0) {
         for (int q = 0; q < 8; ++q) atomicAdd(P.stats + 8 + q, (unsigned long long)ph_acc[q]);
+        for (int q = 8; q < 16; ++q) atomicAdd(P.stats + 16 + q, (unsigned long long)ph_acc[q]);
         atomicAdd(P.stats + 16, (unsigned long long)(__builtin_amdgcn_s_memtime() - kt0));
         atomicAdd(P.stats + 20, (unsigned long long)ph_vis);
         atomicAdd(P.stats + 21, (unsigned long long)ph_cnt[0]);

@@ -363,7 +363,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             return rc;
         c->cap_slots = n;
     }
-    if ((rc = ensure(c, c->counts, 5 * kMaxParts * 4)) || (rc = ensure(c, c->stats, 256))) return rc;
+    if ((rc = ensure(c, c->counts, 5 * kMaxParts * 4)) || (rc = ensure(c, c->stats, 512))) return rc;
     float* fb = d_out;
     if (!fb) {
         if ((rc = ensure(c, c->fb, npix * 3 * sizeof(float)))) return rc;
@@ -427,7 +427,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     };
 
     HIPCHK(c, hipMemsetAsync(fb, 0, npix * 3 * sizeof(float), c->stream));
-    HIPCHK(c, hipMemsetAsync(P.stats, 0, 256, c->stream));
+    HIPCHK(c, hipMemsetAsync(P.stats, 0, 512, c->stream));
     HIPCHK(c, launch(XRT_K_SEED, [&] { return launch_seed(P, lists[0], counts_at(0), counts_at(1), req_counts, c->stream); }));
     // refill epochs: shading launches of epoch e append to req_counts[e & 1]; k_refill(e)
     // consumes it and clears req_counts[(e + 1) & 1] for epoch e + 1.  Epoch 0 is the
@@ -565,8 +565,8 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
         for (uint32_t k = 0; k < P.n_part; ++k)
             if (left[k] != 0) return set_err(c, XRT_ERR_HIP, "iteration cap reached with live paths");
     }
-    unsigned long long hs[32] = {0};
-    HIPCHK(c, hipMemcpy(hs, P.stats, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long hs[40] = {0};
+    HIPCHK(c, hipMemcpy(hs, P.stats, 40 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     if (hs[5] || hs[6]) std::fprintf(stderr, "[xrt] triangle tests: lane %llu wave %llu\n", hs[5], hs[6]);
     if (hs[8] || hs[9]) {   // -DXRT_PHASE_CLOCK experiment builds
         std::fprintf(stderr, "[xrt] phase cycles (sum over waves):");
@@ -575,6 +575,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
                      hs[16], hs[17], hs[18], hs[19], hs[20], hs[21], hs[22], hs[23]);
         std::fprintf(stderr, " | coop closest cull/scan/expand/pass %llu %llu %llu %llu shadow %llu %llu %llu %llu",
                      hs[24], hs[25], hs[26], hs[27], hs[28], hs[29], hs[30], hs[31]);
+        std::fprintf(stderr, " | shade hit/rr/nee/bsdf %llu %llu %llu %llu", hs[32], hs[33], hs[34], hs[35]);
         std::fprintf(stderr, "\n");
     }
     S.segments = hs[0], S.shadow_rays = hs[1], S.draws = hs[2], S.rejected = hs[3], S.stalled = hs[4];
