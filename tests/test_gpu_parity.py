@@ -264,13 +264,18 @@ def test_c3_spheres_direct(renderer, sched):
     assert renderer.stats.shadow_rays == st["shadow_rays"]
 
 
-def test_c4_sphere_mesh_gi(renderer):
-    """Config C4 scene family (Cornell + tessellated sphere) at reduced tessellation/size."""
-    s = scenes.cornell_spheremesh(64, 36, n_theta=24, n_phi=24)
-    img, ref, _ = render_both(renderer, s, 64, 36, 4)
+@pytest.mark.parametrize("nt,w,h,spp", [(24, 64, 36, 4), (80, 48, 30, 3)])
+def test_c4_sphere_mesh_gi(renderer, nt, w, h, spp):
+    """Config C4 scene family (Cornell + tessellated sphere; 1,152 and 12,800 mesh triangles)
+    at reduced size: the wavefront schedule with BVH traces, bit-exact against the oracle's
+    linear scan, counters included."""
+    s = scenes.cornell_spheremesh(w, h, n_theta=nt, n_phi=nt)
+    img, ref, st = render_both(renderer, s, w, h, spp)
     compare(img, ref)
-    assert renderer.stats.launches[abi.XRT_K_STEP] == 0   # too large for LDS: multi-pass schedule
-    assert renderer.stats.schedule == abi.XRT_SCHED_WAVEFRONT
+    g = renderer.stats
+    assert g.launches[abi.XRT_K_STEP] == 0   # too large for LDS: multi-pass schedule
+    assert g.schedule == abi.XRT_SCHED_WAVEFRONT
+    assert (g.segments, g.shadow_rays, g.draws) == (st["segments"], st["shadow_rays"], st["draws"])
 
 
 def test_triangle_light_and_two_lights(renderer, sched):

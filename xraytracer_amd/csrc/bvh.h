@@ -1,0 +1,44 @@
+// bvh.h — host-side bounding volume hierarchy over a scene's primitives (triangles of
+// large triangle scenes, C4), consumed by k_trace_bvh (wavefront.hip).
+//
+// The reference scans every primitive (Scene::intersect, Src/scene.cpp:190-200); the
+// hierarchy only decides which primitives a ray needs to be tested against, and the
+// device keeps the reference's result: closest hit = smallest t, ties to the lowest
+// primitive index (the in-order strict `t < best` scan), any-hit for shadow rays.  Node
+// boxes are padded by a margin far above the float error of a Moller-Trumbore hit
+// position, so a box test never rejects a hit the linear scan accepts.
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+namespace xrt {
+
+// Binary BVH node holding both children's boxes (64 bytes = 4 float4), so one node fetch
+// tests both children: {lmin, left}, {lmax, lcount}, {rmin, right}, {rmax, rcount}.
+// A child with count > 0 is a leaf of `count` primitives starting at `index` of the
+// reordered primitive array; count == 0 is an interior node at `index`; count == -1 is an
+// empty slot (a one-leaf tree's right child).
+struct BvhNode {
+    float lmin[3];
+    int32_t left;
+    float lmax[3];
+    int32_t lcount;
+    float rmin[3];
+    int32_t right;
+    float rmax[3];
+    int32_t rcount;
+};
+
+struct BvhBuild {
+    std::vector<BvhNode> nodes;      // nodes[0] is the root
+    std::vector<uint32_t> order;     // reordered primitive array: order[i] = original index
+    int depth = 0;                   // deepest node (traversal stack bound)
+};
+
+// prim_min / prim_max: n boxes (3 floats each).  Binned SAH, leaves of <= leaf_max
+// primitives, median split below max_depth - 8 levels of headroom; margin pads every box.
+BvhBuild build_bvh(const float* prim_min, const float* prim_max, uint32_t n, uint32_t leaf_max, float margin,
+                   int max_depth);
+
+}  // namespace xrt

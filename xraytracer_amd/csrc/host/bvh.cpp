@@ -1,0 +1,146 @@
+// bvh.cpp — binned-SAH BVH build on the host (see bvh.h).
+#include "../bvh.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <cstring>
+
+namespace xrt {
+
+namespace {
+
+struct Ref {
+    float mn[3], mx[3], c[3];
+    uint32_t idx;
+};
+
+struct Box {
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    void grow(const float* a, const float* b) {
+        for (int q = 0; q < 3; ++q) mn[q] = std::min(mn[q], a[q]), mx[q] = std::max(mx[q], b[q]);
+    }
+    void grow(const Box& o) { grow(o.mn, o.mx); }
+    float area() const {
+        if (mx[0] < mn[0]) return 0.0f;
+        const float dx = mx[0] - mn[0], dy = mx[1] - mn[1], dz = mx[2] - mn[2];
+        return 2.0f * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+struct Builder {
+    std::vector<Ref> refs;
+    BvhBuild out;
+    uint32_t leaf_max;
+    float margin;
+    int max_depth;
+
+    Box bounds(uint32_t lo, uint32_t hi) const {
+        Box b;
+        for (uint32_t i = lo; i < hi; ++i) b.grow(refs[i].mn, refs[i].mx);
+        return b;
+    }
+
+    uint32_t split(uint32_t lo, uint32_t hi, int depth) {
+        const uint32_t n = hi - lo;
+        Box cb;
+        for (uint32_t i = lo; i < hi; ++i) cb.grow(refs[i].c, refs[i].c);
+        int axis = 0;
+        for (int q = 1; q < 3; ++q)
+            if (cb.mx[q] - cb.mn[q] > cb.mx[axis] - cb.mn[axis]) axis = q;
+        const float ext = cb.mx[axis] - cb.mn[axis];
+        auto median = [&]() {
+            const uint32_t mid = lo + n / 2;
+            std::nth_element(refs.begin() + lo, refs.begin() + mid, refs.begin() + hi,
+                             [axis](const Ref& a, const Ref& b) { return a.c[axis] < b.c[axis]; });
+            return mid;
+        };
+        if (!(ext > 0.0f) || depth >= max_depth - 24) return median();
+        constexpr int kBins = 16;
+        Box bb[kBins];
+        uint32_t bc[kBins] = {0};
+        auto bin_of = [&](const Ref& r) {
+            int b = (int)((r.c[axis] - cb.mn[axis]) / ext * kBins);
+            return std::min(std::max(b, 0), kBins - 1);
+        };
+        for (uint32_t i = lo; i < hi; ++i) {
+            const int b = bin_of(refs[i]);
+            bb[b].grow(refs[i].mn, refs[i].mx);
+            ++bc[b];
+        }
+        float best = FLT_MAX;
+        int best_b = -1;
+        for (int s = 1; s < kBins; ++s) {
+            Box l, r;
+            uint32_t nl = 0, nr = 0;
+            for (int b = 0; b < s; ++b) l.grow(bb[b]), nl += bc[b];
+            for (int b = s; b < kBins; ++b) r.grow(bb[b]), nr += bc[b];
+            if (!nl || !nr) continue;
+            const float cost = l.area() * nl + r.area() * nr;
+            if (cost < best) best = cost, best_b = s;
+        }
+        if (best_b < 0) return median();
+        const auto it = std::partition(refs.begin() + lo, refs.begin() + hi,
+                                       [&](const Ref& r) { return bin_of(r) < best_b; });
+        const uint32_t mid = (uint32_t)(it - refs.begin());
+        return (mid == lo || mid == hi) ? median() : mid;
+    }
+
+    void set_child(float* cmn, float* cmx, int32_t& index, int32_t& count, uint32_t lo, uint32_t hi, int depth) {
+        const Box b = bounds(lo, hi);
+        for (int q = 0; q < 3; ++q) cmn[q] = b.mn[q] - margin, cmx[q] = b.mx[q] + margin;
+        if (hi - lo <= leaf_max) {
+            index = (int32_t)lo;
+            count = (int32_t)(hi - lo);
+            out.depth = std::max(out.depth, depth);
+        } else {
+            index = (int32_t)node(lo, hi, depth);
+            count = 0;
+        }
+    }
+
+    uint32_t node(uint32_t lo, uint32_t hi, int depth) {
+        const uint32_t id = (uint32_t)out.nodes.size();
+        out.nodes.push_back(BvhNode{});
+        out.depth = std::max(out.depth, depth);
+        const uint32_t mid = split(lo, hi, depth);
+        BvhNode nd{};
+        set_child(nd.lmin, nd.lmax, nd.left, nd.lcount, lo, mid, depth + 1);
+        set_child(nd.rmin, nd.rmax, nd.right, nd.rcount, mid, hi, depth + 1);
+        out.nodes[id] = nd;
+        return id;
+    }
+};
+
+}  // namespace
+
+BvhBuild build_bvh(const float* prim_min, const float* prim_max, uint32_t n, uint32_t leaf_max, float margin,
+                   int max_depth) {
+    Builder B;
+    B.leaf_max = std::max<uint32_t>(1u, leaf_max);
+    B.margin = margin;
+    B.max_depth = max_depth;
+    B.refs.resize(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        Ref& r = B.refs[i];
+        for (int q = 0; q < 3; ++q) {
+            r.mn[q] = prim_min[3 * i + q], r.mx[q] = prim_max[3 * i + q];
+            r.c[q] = 0.5f * (r.mn[q] + r.mx[q]);
+        }
+        r.idx = i;
+    }
+    if (n <= B.leaf_max) {
+        BvhNode root{};
+        B.set_child(root.lmin, root.lmax, root.left, root.lcount, 0, n, 1);
+        if (n == 0) root.lcount = -1;
+        root.right = 0, root.rcount = -1;
+        for (int q = 0; q < 3; ++q) root.rmin[q] = FLT_MAX, root.rmax[q] = -FLT_MAX;
+        B.out.nodes.push_back(root);
+    } else {
+        B.node(0, n, 0);
+    }
+    B.out.order.resize(n);
+    for (uint32_t i = 0; i < n; ++i) B.out.order[i] = B.refs[i].idx;
+    return std::move(B.out);
+}
+
+}  // namespace xrt

@@ -91,6 +91,8 @@ struct StepObjs {
     StepObj o[kMergedMaxObjs];
     int n;
 };
+constexpr uint32_t kBvhLeaf = 4;      // BVH: primitives per leaf (at most)
+constexpr int kBvhMaxDepth = 48;      // BVH: depth bound = traversal stack entries
 constexpr int kSmallTris = 1024;   // scenes up to this size keep every triangle in LDS
 constexpr int kSmallObjs = 256;
 constexpr unsigned kStepLds = 64u * 1024u;   // LDS budget of the fused schedule (k_step)
@@ -126,6 +128,8 @@ struct KParams {
     const DLight* lights;
     const DSeg* segs;
     const DObjBox* obj_box;   // per object, for the small-scene trace path (n_objs entries)
+    const f4* bvh_node;       // large triangle scenes: BvhNode array (4 f4 each, bvh.h), else null
+    const f4* bvh_tri;        // triangles in BVH leaf order, as `tri` but e2.w = original index
     int n_segs, n_lights, n_tris, n_sph, n_box, scene_kind, n_objs, small_tri;
     DMedium medium;
     // ---- camera (row-major c2w) + PinholeCamera scale / aspect

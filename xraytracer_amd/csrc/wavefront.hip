@@ -218,6 +218,119 @@ __global__ __launch_bounds__(kBlock) void k_trace(KParams P, const uint32_t* __r
     }
 }
 
+// ====================================================================== BVH trace ====
+// Large triangle scenes (C4): closest hit and any-hit through the host-built BVH (bvh.h).
+// Exactness: every node box is padded beyond the float error of a Moller-Trumbore hit, a
+// child is entered when its box overlaps [0, best t] (inclusive: a later triangle at the
+// same t with a lower index must still be found), and the closest hit is the
+// lexicographic minimum of (t, original index) — the reference's in-order strict
+// `t < best` scan over all triangles (Src/scene.cpp:190-200, primitive.cpp:83-131).
+// Shadow rays test occluder triangles only and stop at the first hit (Scene::occluded).
+// One ray per lane; the traversal stack lives in LDS (kBvhMaxDepth entries per thread).
+__device__ __forceinline__ bool bvh_box(const f4& mn, const f4& mx, v3 o, v3 inv, float tlim) {
+    const float tx0 = (mn.x - o.x) * inv.x, tx1 = (mx.x - o.x) * inv.x;
+    const float ty0 = (mn.y - o.y) * inv.y, ty1 = (mx.y - o.y) * inv.y;
+    const float tz0 = (mn.z - o.z) * inv.z, tz1 = (mx.z - o.z) * inv.z;
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
+    return !(tn > tf);
+}
+
+template <bool ANY>
+__device__ __forceinline__ bool bvh_leaf(const KParams& P, int first, int count, v3 o, v3 d, float tmax, float& bt,
+                                         float& bu, float& bv, int& bk) {
+    for (int i = first; i < first + count; ++i) {
+        const f4 A = P.bvh_tri[3 * i], B = P.bvh_tri[3 * i + 1], C = P.bvh_tri[3 * i + 2];
+        if (ANY && B.w == 0.0f) continue;   // area-light objects never occlude
+        float t, u, v;
+        if (!ray_tri(o, d, xyz(A), xyz(B), xyz(C), t, u, v)) continue;
+        if (ANY) {
+            if (t < tmax) return true;
+        } else {
+            const int k = __float_as_int(C.w);
+            if (t < bt || (t == bt && k < bk)) bt = t, bu = u, bv = v, bk = k;
+        }
+    }
+    return false;
+}
+
+// ANY: returns occluded; else fills (bt, bu, bv, bk) (bk = -1: miss)
+template <bool ANY>
+__device__ bool bvh_trace(const KParams& P, uint32_t* stk, v3 o, v3 d, float tmax, float& bt, float& bu, float& bv,
+                          int& bk) {
+    const v3 inv = rcp3(d);
+    int sp = 0;
+    int node = 0;
+    while (true) {
+        const f4* N = P.bvh_node + 4 * (size_t)node;
+        const f4 n0 = N[0], n1 = N[1], n2 = N[2], n3 = N[3];
+        const float lim = ANY ? tmax : bt;
+        const int lcount = __float_as_int(n1.w), rcount = __float_as_int(n3.w);
+        const bool hl = lcount >= 0 && bvh_box(n0, n1, o, inv, lim);
+        const bool hr = rcount >= 0 && bvh_box(n2, n3, o, inv, lim);
+        int next = -1;
+        if (hl) {
+            if (lcount > 0) {
+                if (bvh_leaf<ANY>(P, __float_as_int(n0.w), lcount, o, d, tmax, bt, bu, bv, bk)) return true;
+            } else {
+                next = __float_as_int(n0.w);
+            }
+        }
+        if (hr) {
+            if (rcount > 0) {
+                if (bvh_leaf<ANY>(P, __float_as_int(n2.w), rcount, o, d, tmax, bt, bu, bv, bk)) return true;
+            } else if (next < 0) {
+                next = __float_as_int(n2.w);
+            } else {
+                stk[(sp++) * kBlock] = (uint32_t)__float_as_int(n2.w);
+            }
+        }
+        if (next >= 0) {
+            node = next;
+        } else {
+            if (sp == 0) break;
+            node = (int)stk[(--sp) * kBlock];
+        }
+    }
+    return false;
+}
+
+template <int NL>
+__global__ __launch_bounds__(kBlock) void k_trace_bvh(KParams P, const uint32_t* __restrict__ list,
+                                                       const uint32_t* __restrict__ count, uint32_t* zero_count) {
+    __shared__ uint32_t stack[kBvhMaxDepth * kBlock];
+    zero_parts(P, zero_count);
+    const PartIter it = part_iter(P, count, kBlock);
+    const int tid = threadIdx.x;
+    uint32_t* stk = stack + tid;
+    for (uint32_t base = it.first; base < it.n; base += it.stride) {
+        const uint32_t i = base + tid;
+        if (i >= it.n) continue;
+        const uint32_t s = list[it.p * P.part_cap + i];
+        const uint32_t st = P.state[s];
+        const uint32_t smask = (st >> ST_SHADOW_SHIFT) & ((1u << NL) - 1u);
+        if (st & ST_RAY) {
+            float bt = kINF, bu = 0.0f, bv = 0.0f;
+            int bk = -1;
+            (void)bvh_trace<false>(P, stk, xyz(P.ray_o[s]), xyz(P.ray_d[s]), kINF, bt, bu, bv, bk);
+            P.hit[s] = make_float4(bt, bu, bv, __int_as_float(bk));
+        }
+        if (smask) {
+            uint32_t occ = 0;
+#pragma unroll
+            for (int l = 0; l < NL; ++l) {
+                if (!(smask & (1u << l))) continue;
+                const f4 a = P.sh_o[(size_t)l * P.n_slots + s];
+                float bt = kINF, bu, bv;
+                int bk = -1;
+                if (bvh_trace<true>(P, stk, xyz(a), xyz(P.sh_d[(size_t)l * P.n_slots + s]), a.w, bt, bu, bv, bk))
+                    occ |= 1u << l;
+            }
+            P.occ[s] = occ;
+        }
+    }
+}
+
 // Small triangle scenes (<= kSmallTris triangles, e.g. the Cornell box): every triangle
 // and the per-object boxes live in LDS for the whole launch; objects are visited in
 // Scene iteration order and a wave skips an object none of its rays can hit (closest-hit
@@ -1702,6 +1815,13 @@ static hipError_t trace_nl(const KParams& P, const uint32_t* list, const uint32_
 
 hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
                         uint32_t blocks, hipStream_t st) {
+    if (P.bvh_node && P.scene_kind == SCN_TRI) {
+        if (P.n_lights <= 1)
+            hipLaunchKernelGGL((k_trace_bvh<1>), dim3(blocks), dim3(kBlock), 0, st, P, list, count, zero);
+        else
+            hipLaunchKernelGGL((k_trace_bvh<kMaxLights>), dim3(blocks), dim3(kBlock), 0, st, P, list, count, zero);
+        return hipGetLastError();
+    }
     if (P.small_tri) {
         const size_t lds = (size_t)P.n_tris * 3 * sizeof(f4) + (size_t)P.n_objs * sizeof(DObjBox);
         if (P.n_lights <= 1)

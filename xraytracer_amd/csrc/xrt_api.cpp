@@ -9,9 +9,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <cfloat>
 #include <string>
 #include <vector>
 
+#include "bvh.h"
 #include "launch.h"
 #include "wavefront.h"
 #include "xrt.h"
@@ -36,7 +38,7 @@ struct xrt_ctx {
     std::string err;
     // scene
     std::vector<DevBuf*> scene_bufs;
-    DevBuf tri, tri_ng, tri_nrm, sph, sph_obj, box, objs, lights, segs, density, obj_box;
+    DevBuf tri, tri_ng, tri_nrm, sph, sph_obj, box, objs, lights, segs, density, obj_box, bvh_node, bvh_tri;
     KParams base{};
     StepObjs step_objs{};   // kernel-argument object records of the merged-trace schedule
     bool has_scene = false, has_camera = false, has_medium = false;
@@ -135,7 +137,7 @@ void xrt_destroy(xrt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->tri, &c->tri_ng, &c->tri_nrm, &c->sph, &c->sph_obj, &c->box, &c->objs, &c->lights,
-                     &c->segs, &c->density, &c->obj_box, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
+                     &c->segs, &c->density, &c->obj_box, &c->bvh_node, &c->bvh_tri, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
                      &c->hit2, &c->hit3, &c->sh_o, &c->sh_d, &c->sh_c, &c->med, &c->med2, &c->state,
                      &c->sample_k, &c->depth, &c->occ, &c->rng_c, &c->rng_g, &c->ring, &c->c_seg, &c->c_shadow,
                      &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch, &c->kparams};
@@ -290,6 +292,39 @@ int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
         P.obj_box = as<DObjBox>(c->obj_box);
         if (boxes.size() <= (size_t)kMergedMaxObjs) build_step_objs(boxes.data(), (int)boxes.size(), c->step_objs);
         P.small_tri = 1;
+    }
+    // large triangle scenes: a BVH for the wavefront trace (C4's 51k-triangle sphere mesh).
+    // Margin: 1e-4 of the scene diagonal + 1e-4, above the float error of a Moller-Trumbore
+    // hit position, so box tests never drop a hit the linear scan accepts.
+    P.bvh_node = nullptr, P.bvh_tri = nullptr;
+    if (P.scene_kind == SCN_TRI && !P.small_tri && P.n_tris > 0 && !std::getenv("XRT_NO_BVH")) {
+        const size_t nt = (size_t)P.n_tris;
+        std::vector<float> mn(3 * nt), mx(3 * nt);
+        float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (size_t t = 0; t < nt; ++t) {
+            const f4 v0 = tri[3 * t], e1 = tri[3 * t + 1], e2 = tri[3 * t + 2];
+            const float vs[3][3] = {{v0.x, v0.y, v0.z}, {v0.x + e1.x, v0.y + e1.y, v0.z + e1.z},
+                                    {v0.x + e2.x, v0.y + e2.y, v0.z + e2.z}};
+            for (int q = 0; q < 3; ++q) {
+                mn[3 * t + q] = std::min({vs[0][q], vs[1][q], vs[2][q]});
+                mx[3 * t + q] = std::max({vs[0][q], vs[1][q], vs[2][q]});
+                lo[q] = std::min(lo[q], mn[3 * t + q]), hi[q] = std::max(hi[q], mx[3 * t + q]);
+            }
+        }
+        const float diag = std::sqrt((hi[0] - lo[0]) * (hi[0] - lo[0]) + (hi[1] - lo[1]) * (hi[1] - lo[1]) +
+                                     (hi[2] - lo[2]) * (hi[2] - lo[2]));
+        const BvhBuild B = build_bvh(mn.data(), mx.data(), (uint32_t)nt, kBvhLeaf, 1e-4f * diag + 1e-4f, kBvhMaxDepth);
+        if (B.depth >= kBvhMaxDepth) return set_err(c, XRT_ERR_UNSUPPORTED, "BVH deeper than the traversal stack");
+        std::vector<f4> btri(3 * nt);
+        for (size_t i = 0; i < nt; ++i) {
+            const uint32_t t = B.order[i];
+            btri[3 * i] = tri[3 * t], btri[3 * i + 1] = tri[3 * t + 1], btri[3 * i + 2] = tri[3 * t + 2];
+            btri[3 * i + 2].w = bits((int)t);
+        }
+        if ((rc = upload(c, c->bvh_node, B.nodes.data(), B.nodes.size() * sizeof(BvhNode))) ||
+            (rc = upload(c, c->bvh_tri, btri.data(), btri.size() * sizeof(f4))))
+            return rc;
+        P.bvh_node = as<f4>(c->bvh_node), P.bvh_tri = as<f4>(c->bvh_tri);
     }
     c->has_scene = true;
     return XRT_OK;
