@@ -264,6 +264,33 @@ def test_c3_spheres_direct(renderer, sched):
     assert renderer.stats.shadow_rays == st["shadow_rays"]
 
 
+def dup_spheres(w, h):
+    """Sphere scene with every sphere present twice (same centre and radius, different
+    albedo): equal hit distances, so the sphere BVH must reproduce the reference's
+    in-order tie break (the first object in iteration order wins)."""
+    s = scenes.SceneBundle()
+    for k in range(24):
+        x, z = -3.0 + (k % 6) * 1.2, -2.0 - (k // 6) * 1.2
+        s.add_sphere(f"a{k:02d}", (x, 0.0, z), 0.5, (0.9, 0.2, 0.2))
+        s.add_sphere(f"b{k:02d}", (x, 0.0, z), 0.5, (0.2, 0.9, 0.2))
+    s.add_sphere_light("SphereLight", (0.0, 6.0, -4.0), 1.5, (20.0, 20.0, 20.0))
+    s.flatten()
+    s.camera = scenes.pinhole((1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 3, 4, 1), 60.0, w, h)
+    s.integrator, s.max_depth = "gi", 3
+    return s
+
+
+@pytest.mark.parametrize("integ", ["direct", "gi"])
+def test_sphere_bvh_ties_and_gi(renderer, sched, integ):
+    """Sphere BVH (fused schedule) vs the oracle's linear scan: duplicated spheres (ties
+    broken by iteration order), GI bounces between spheres, Direct."""
+    s = dup_spheres(64, 48)
+    img, ref, st = render_both(renderer, s, 64, 48, 4, integrator=integ, schedule=sched)
+    compare(img, ref)
+    assert renderer.stats.segments == st["segments"]
+    assert renderer.stats.shadow_rays == st["shadow_rays"]
+
+
 @pytest.mark.parametrize("nt,w,h,spp", [(24, 64, 36, 4), (80, 48, 30, 3)])
 def test_c4_sphere_mesh_gi(renderer, nt, w, h, spp):
     """Config C4 scene family (Cornell + tessellated sphere; 1,152 and 12,800 mesh triangles)

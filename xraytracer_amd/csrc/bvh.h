@@ -36,6 +36,18 @@ struct BvhBuild {
     int depth = 0;                   // deepest node (traversal stack bound)
 };
 
+// Threaded ("skip-link") form of a BvhBuild for stackless traversal: nodes in depth-first
+// order, one box each; a ray that overlaps node i continues at i + 1 (its first child, or
+// the next subtree after a leaf), a ray that misses it jumps to `skip` (the node after
+// i's whole subtree).  leaf = -1 for an interior node, else (count << 24) | first.
+struct SkipNode {
+    float bmin[3];
+    int32_t skip;
+    float bmax[3];
+    int32_t leaf;
+};
+std::vector<SkipNode> thread_bvh(const BvhBuild& b);
+
 // prim_min / prim_max: n boxes (3 floats each).  Binned SAH, leaves of <= leaf_max
 // primitives, median split below max_depth - 8 levels of headroom; margin pads every box.
 BvhBuild build_bvh(const float* prim_min, const float* prim_max, uint32_t n, uint32_t leaf_max, float margin,

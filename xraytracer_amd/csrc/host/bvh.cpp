@@ -143,4 +143,31 @@ BvhBuild build_bvh(const float* prim_min, const float* prim_max, uint32_t n, uin
     return std::move(B.out);
 }
 
+namespace {
+void emit_child(const BvhBuild& b, std::vector<SkipNode>& out, const float* mn, const float* mx, int32_t index,
+                int32_t count) {
+    if (count < 0) return;   // empty slot
+    const size_t me = out.size();
+    SkipNode s{};
+    for (int q = 0; q < 3; ++q) s.bmin[q] = mn[q], s.bmax[q] = mx[q];
+    s.leaf = count > 0 ? (int32_t)(((uint32_t)count << 24) | (uint32_t)index) : -1;
+    out.push_back(s);
+    if (count == 0) {
+        const BvhNode& n = b.nodes[(size_t)index];
+        emit_child(b, out, n.lmin, n.lmax, n.left, n.lcount);
+        emit_child(b, out, n.rmin, n.rmax, n.right, n.rcount);
+    }
+    out[me].skip = (int32_t)out.size();
+}
+}  // namespace
+
+std::vector<SkipNode> thread_bvh(const BvhBuild& b) {
+    std::vector<SkipNode> out;
+    if (b.nodes.empty()) return out;
+    const BvhNode& r = b.nodes[0];
+    emit_child(b, out, r.lmin, r.lmax, r.left, r.lcount);
+    emit_child(b, out, r.rmin, r.rmax, r.right, r.rcount);
+    return out;
+}
+
 }  // namespace xrt

@@ -373,20 +373,27 @@ __device__ __forceinline__ void camera_ray(const KParams& P, float u, float v, v
 // geometric and vertex normals, per-object culling boxes (triangle scenes), spheres,
 // medium boxes, the object and light tables, sphere->object map.
 struct StepLayout {
-    uint32_t tri, tng, nrm, box, sph, bx, obj, light, sobj, total;
+    uint32_t tri, tng, nrm, box, sph, bx, obj, light, sobj, snode, ssph, sbk, total;
 };
+// Sphere scenes with a skip-link BVH (P.n_snode > 0, C3) keep the BVH, the spheres in leaf
+// order and their index/occluder words in LDS; the original-order sphere, sphere-object
+// and object tables (read once per hit, at shading) stay in global memory.
 __host__ __device__ inline StepLayout step_layout(const KParams& P) {
+    const bool sb = P.n_snode > 0;
     StepLayout L;
     L.tri = 0;
     L.tng = L.tri + 48u * P.n_tris;
     L.nrm = L.tng + 16u * P.n_tris;
     L.box = L.nrm + 48u * P.n_tris;
     L.sph = L.box + (P.scene_kind == SCN_TRI ? 32u * P.n_objs : 0u);
-    L.bx = L.sph + 16u * P.n_sph;
+    L.bx = L.sph + (sb ? 0u : 16u * P.n_sph);
     L.obj = L.bx + 32u * P.n_box;
-    L.light = L.obj + (uint32_t)sizeof(DObj) * P.n_objs;
+    L.light = L.obj + (sb ? 0u : (uint32_t)sizeof(DObj) * P.n_objs);
     L.sobj = L.light + (uint32_t)sizeof(DLight) * P.n_lights;
-    L.total = L.sobj + 4u * P.n_sph;
+    L.snode = L.sobj + (sb ? 0u : 4u * P.n_sph);
+    L.ssph = L.snode + 32u * (uint32_t)P.n_snode;
+    L.sbk = L.ssph + (sb ? 16u * P.n_sph : 0u);
+    L.total = L.sbk + (sb ? 4u * P.n_sph : 0u);
     return L;
 }
 
@@ -410,6 +417,10 @@ struct LScene {
     const f4* bx;       // 2 per box
     const DObj* obj;
     const DLight* light;
+    const f4* snode = nullptr;   // sphere BVH (SkipNode: {bmin, skip}, {bmax, leaf}); n_snode > 0
+    const f4* ssph = nullptr;    // spheres in BVH leaf order
+    const int* sbk = nullptr;    // original sphere index | (occluder << 30)
+    int n_snode = 0;
 };
 
 

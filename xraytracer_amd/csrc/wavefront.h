@@ -93,6 +93,7 @@ struct StepObjs {
 };
 constexpr uint32_t kBvhLeaf = 4;      // BVH: primitives per leaf (at most)
 constexpr int kBvhMaxDepth = 48;      // BVH: depth bound = traversal stack entries
+constexpr int kSphBvhMin = 16;        // sphere scenes with at least this many spheres get a skip-link BVH
 constexpr int kSmallTris = 1024;   // scenes up to this size keep every triangle in LDS
 constexpr int kSmallObjs = 256;
 constexpr unsigned kStepLds = 64u * 1024u;   // LDS budget of the fused schedule (k_step)
@@ -130,6 +131,10 @@ struct KParams {
     const DObjBox* obj_box;   // per object, for the small-scene trace path (n_objs entries)
     const f4* bvh_node;       // large triangle scenes: BvhNode array (4 f4 each, bvh.h), else null
     const f4* bvh_tri;        // triangles in BVH leaf order, as `tri` but e2.w = original index
+    const f4* snode;          // sphere scenes: threaded BVH (bvh.h SkipNode, 2 f4 each), else null
+    const f4* ssph;           // spheres in BVH leaf order (center, radius)
+    const int* sbk;           // per ssph entry: original sphere index | (occluder << 30)
+    int n_snode;
     int n_segs, n_lights, n_tris, n_sph, n_box, scene_kind, n_objs, small_tri;
     DMedium medium;
     // ---- camera (row-major c2w) + PinholeCamera scale / aspect

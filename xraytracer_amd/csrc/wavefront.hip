@@ -888,6 +888,45 @@ struct HitRec {
     float st, su, sv, du, dv, t1;
 };
 
+// Sphere scenes (C3): stackless traversal of the threaded BVH (bvh.h SkipNode) in LDS.
+// Same exactness argument as the triangle BVH: boxes are the spheres' bounds padded far
+// beyond the float error of Sphere::intersect's hit point, a box is entered when it
+// overlaps [0, best t] (inclusive), and the closest hit is the lexicographic minimum of
+// (t, original index) — the reference's in-order strict `t < best` scan over the objects
+// (Src/scene.cpp:190-200, primitive.h:106-124).  Any-hit for shadow rays skips spheres of
+// area-light objects (Scene::occluded, Src/scene.cpp:202-211).
+template <bool ANY>
+__device__ __forceinline__ bool sphere_bvh(const LScene& L, v3 o, v3 d, float tmax, float& bt, int& bk) {
+    const v3 inv = rcp3(d);
+    int i = 0;
+    while (i < L.n_snode) {
+        const f4 a = L.snode[2 * i], b = L.snode[2 * i + 1];
+        if (!bvh_box(a, b, o, inv, ANY ? tmax : bt)) {
+            i = __float_as_int(a.w);
+            continue;
+        }
+        const int leaf = __float_as_int(b.w);
+        if (leaf >= 0) {
+            const int first = leaf & 0xffffff, end = first + (leaf >> 24);
+            for (int j = first; j < end; ++j) {
+                const int kw = L.sbk[j];
+                if (ANY && !(kw & (1 << 30))) continue;
+                const f4 S = L.ssph[j];
+                float t;
+                if (!sphere_hit(o, d, xyz(S), S.w, t)) continue;
+                if (ANY) {
+                    if (t < tmax) return true;
+                } else {
+                    const int k = kw & 0x3fffffff;
+                    if (t < bt || (t == bt && k < bk)) bt = t, bk = k;
+                }
+            }
+        }
+        ++i;
+    }
+    return false;
+}
+
 // Scene::intersect over the LDS scene (Src/scene.cpp:190-200)
 template <int SCN>
 __device__ __forceinline__ void closest_l(const KParams& P, const LScene& L, v3 o, v3 d, HitRec& h CNT_PARAM) {
@@ -909,6 +948,13 @@ __device__ __forceinline__ void closest_l(const KParams& P, const LScene& L, v3 
             }
         }
     } else if (SCN == SCN_SPHERE) {
+        if (L.n_snode > 0) {
+            float bt = kINF;
+            int bk = -1;
+            (void)sphere_bvh<false>(L, o, d, kINF, bt, bk);
+            if (bk >= 0) h.t = bt, h.code = (1 << 28) | bk;
+            return;
+        }
         for (int k = 0; k < P.n_sph; ++k) {
             const f4 S = L.sph[k];
             float t;
@@ -963,6 +1009,11 @@ __device__ __forceinline__ bool occluded_l(const KParams& P, const LScene& L, v3
         }
         return false;
     } else {
+        if (SCN == SCN_SPHERE && L.n_snode > 0) {
+            float bt = kINF;
+            int bk = -1;
+            return sphere_bvh<true>(L, o, d, tmax, bt, bk);
+        }
         for (int sg = 0; sg < P.n_segs; ++sg) {
             const DSeg seg = P.segs[sg];
             if (SCN == SCN_MIXED && seg.kind == SEG_TRI) {
@@ -1040,11 +1091,23 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
     lds_copy(const_cast<f4*>(L.tng), P.tri_ng, P.n_tris, tid);
     lds_copy(const_cast<f4*>(L.nrm), P.tri_nrm, 3 * P.n_tris, tid);
     if (SCN == SCN_TRI) lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid);
-    lds_copy(const_cast<f4*>(L.sph), P.sph, P.n_sph, tid);
     lds_copy(const_cast<f4*>(L.bx), P.box, 2 * P.n_box, tid);
-    lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
     lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid);
-    lds_copy(const_cast<int*>(L.sobj), P.sph_obj, P.n_sph, tid);
+    if (SCN == SCN_SPHERE && P.n_snode > 0) {
+        // sphere BVH in LDS; per-hit tables read from global memory (step_layout)
+        L.snode = reinterpret_cast<const f4*>(lb + Lo.snode);
+        L.ssph = reinterpret_cast<const f4*>(lb + Lo.ssph);
+        L.sbk = reinterpret_cast<const int*>(lb + Lo.sbk);
+        L.n_snode = P.n_snode;
+        lds_copy(const_cast<f4*>(L.snode), P.snode, 2 * P.n_snode, tid);
+        lds_copy(const_cast<f4*>(L.ssph), P.ssph, P.n_sph, tid);
+        lds_copy(const_cast<int*>(L.sbk), P.sbk, P.n_sph, tid);
+        L.sph = P.sph, L.sobj = P.sph_obj, L.obj = P.objs;
+    } else {
+        lds_copy(const_cast<f4*>(L.sph), P.sph, P.n_sph, tid);
+        lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
+        lds_copy(const_cast<int*>(L.sobj), P.sph_obj, P.n_sph, tid);
+    }
     __syncthreads();
     zero_parts(P, zero_count);
     const int lane = tid & 63;

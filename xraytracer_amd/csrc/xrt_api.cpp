@@ -38,7 +38,8 @@ struct xrt_ctx {
     std::string err;
     // scene
     std::vector<DevBuf*> scene_bufs;
-    DevBuf tri, tri_ng, tri_nrm, sph, sph_obj, box, objs, lights, segs, density, obj_box, bvh_node, bvh_tri;
+    DevBuf tri, tri_ng, tri_nrm, sph, sph_obj, box, objs, lights, segs, density, obj_box, bvh_node, bvh_tri, snode,
+        ssph, sbk;
     KParams base{};
     StepObjs step_objs{};   // kernel-argument object records of the merged-trace schedule
     bool has_scene = false, has_camera = false, has_medium = false;
@@ -137,7 +138,7 @@ void xrt_destroy(xrt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->tri, &c->tri_ng, &c->tri_nrm, &c->sph, &c->sph_obj, &c->box, &c->objs, &c->lights,
-                     &c->segs, &c->density, &c->obj_box, &c->bvh_node, &c->bvh_tri, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
+                     &c->segs, &c->density, &c->obj_box, &c->bvh_node, &c->bvh_tri, &c->snode, &c->ssph, &c->sbk, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
                      &c->hit2, &c->hit3, &c->sh_o, &c->sh_d, &c->sh_c, &c->med, &c->med2, &c->state,
                      &c->sample_k, &c->depth, &c->occ, &c->rng_c, &c->rng_g, &c->ring, &c->c_seg, &c->c_shadow,
                      &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch, &c->kparams};
@@ -325,6 +326,40 @@ int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
             (rc = upload(c, c->bvh_tri, btri.data(), btri.size() * sizeof(f4))))
             return rc;
         P.bvh_node = as<f4>(c->bvh_node), P.bvh_tri = as<f4>(c->bvh_tri);
+    }
+    // sphere scenes (C3's 1001 spheres): a threaded BVH for the fused schedule's traces.
+    // Sphere boxes: center +- radius, padded by 1e-4 of the scene diagonal + 1e-4 —
+    // far above the float error of Sphere::intersect's hit point (and of its
+    // near-tangent discriminant), so a box test never drops a hit the linear scan accepts.
+    P.snode = nullptr, P.ssph = nullptr, P.sbk = nullptr, P.n_snode = 0;
+    if (P.scene_kind == SCN_SPHERE && P.n_sph >= kSphBvhMin && !std::getenv("XRT_NO_BVH")) {
+        const size_t ns = (size_t)P.n_sph;
+        std::vector<float> mn(3 * ns), mx(3 * ns);
+        float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (size_t k = 0; k < ns; ++k) {
+            const float cc[3] = {sph[k].x, sph[k].y, sph[k].z}, r = std::fabs(sph[k].w);
+            for (int q = 0; q < 3; ++q) {
+                mn[3 * k + q] = cc[q] - r, mx[3 * k + q] = cc[q] + r;
+                lo[q] = std::min(lo[q], mn[3 * k + q]), hi[q] = std::max(hi[q], mx[3 * k + q]);
+            }
+        }
+        const float diag = std::sqrt((hi[0] - lo[0]) * (hi[0] - lo[0]) + (hi[1] - lo[1]) * (hi[1] - lo[1]) +
+                                     (hi[2] - lo[2]) * (hi[2] - lo[2]));
+        const BvhBuild B = build_bvh(mn.data(), mx.data(), (uint32_t)ns, kBvhLeaf, 1e-4f * diag + 1e-4f, kBvhMaxDepth);
+        const std::vector<SkipNode> T = thread_bvh(B);
+        std::vector<f4> bs(ns);
+        std::vector<int> bk(ns);
+        for (size_t i = 0; i < ns; ++i) {
+            const uint32_t k = B.order[i];
+            bs[i] = sph[k];
+            bk[i] = (int)k | (sph_obj[k] & (1 << 30));
+        }
+        if ((rc = upload(c, c->snode, T.data(), T.size() * sizeof(SkipNode))) ||
+            (rc = upload(c, c->ssph, bs.data(), bs.size() * sizeof(f4))) ||
+            (rc = upload(c, c->sbk, bk.data(), bk.size() * sizeof(int))))
+            return rc;
+        P.snode = as<f4>(c->snode), P.ssph = as<f4>(c->ssph), P.sbk = as<int>(c->sbk);
+        P.n_snode = (int)T.size();
     }
     c->has_scene = true;
     return XRT_OK;
