@@ -174,12 +174,13 @@ def main():
                     "algorithmic_bytes_per_launch": round(per_launch, 1),
                     "bytes_per_sample": round(b_s, 2), "model": "SURVEY.md 8d: B_s = 68 + 264*Q + 12*D"}
             # secondary: the reference's brute-force triangle tests (every object, every
-            # triangle; shadow rays skip area-light objects) x FLOP_PER_TRI_TEST
+            # triangle; shadow rays skip area-light objects) x FLOP_PER_TRI_TEST — only for
+            # the small triangle scenes whose traces are (culled) linear scans
             d = scene.desc
             n_occ = sum(d.objects[i].count for i in range(d.n_objects)
                         if d.objects[i].kind == abi.XRT_OBJ_MESH and d.objects[i].light < 0)
             tests = (agg["segments"] * d.n_tris + agg["shadow_rays"] * n_occ) / max(1, world)
-            if tests:
+            if tests and d.n_tris <= 1024:   # linear scans only (larger scenes trace a BVH)
                 tf = tests * FLOP_PER_TRI_TEST / (kms[dom] / 1e3) / 1e12
                 roof["valu"] = {"tri_tests_per_sample": round(tests / max(1, samples), 2),
                                 "achieved_tflops": round(tf, 3), "peak_tflops": FP32_PEAK_TFLOPS,

@@ -92,7 +92,8 @@ struct StepObjs {
     int n;
 };
 constexpr uint32_t kBvhLeaf = 4;      // BVH: primitives per leaf (at most)
-constexpr int kBvhMaxDepth = 48;      // BVH: depth bound = traversal stack entries
+constexpr int kBvhMaxDepth = 48;      // BVH build: depth bound (SAH above max - 24 levels, median below)
+constexpr int kBvhStack = 24;         // k_trace_bvh: LDS traversal stack entries per thread (> tree depth)
 constexpr int kSphBvhMin = 16;        // sphere scenes with at least this many spheres get a skip-link BVH
 constexpr int kSmallTris = 1024;   // scenes up to this size keep every triangle in LDS
 constexpr int kSmallObjs = 256;

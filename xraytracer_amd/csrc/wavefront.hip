@@ -226,7 +226,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(KParams P, const uint32_t* __r
 // lexicographic minimum of (t, original index) — the reference's in-order strict
 // `t < best` scan over all triangles (Src/scene.cpp:190-200, primitive.cpp:83-131).
 // Shadow rays test occluder triangles only and stop at the first hit (Scene::occluded).
-// One ray per lane; the traversal stack lives in LDS (kBvhMaxDepth entries per thread).
+// One ray per lane; the traversal stack lives in LDS (kBvhStack entries per thread).
 __device__ __forceinline__ bool bvh_box(const f4& mn, const f4& mx, v3 o, v3 inv, float tlim) {
     const float tx0 = (mn.x - o.x) * inv.x, tx1 = (mx.x - o.x) * inv.x;
     const float ty0 = (mn.y - o.y) * inv.y, ty1 = (mx.y - o.y) * inv.y;
@@ -254,7 +254,20 @@ __device__ __forceinline__ bool bvh_leaf(const KParams& P, int first, int count,
     return false;
 }
 
-// ANY: returns occluded; else fills (bt, bu, bv, bk) (bk = -1: miss)
+// entry distance of the ray segment [0, tlim] into a padded node box, +inf if it misses
+__device__ __forceinline__ float bvh_enter(const f4& mn, const f4& mx, v3 o, v3 inv, float tlim) {
+    const float tx0 = (mn.x - o.x) * inv.x, tx1 = (mx.x - o.x) * inv.x;
+    const float ty0 = (mn.y - o.y) * inv.y, ty1 = (mx.y - o.y) * inv.y;
+    const float tz0 = (mn.z - o.z) * inv.z, tz1 = (mx.z - o.z) * inv.z;
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
+    return tn > tf ? __builtin_inff() : tn;
+}
+
+// ANY: returns occluded; else fills (bt, bu, bv, bk) (bk = -1: miss).  Closest-hit rays
+// descend into the nearer child first (entry distance) and stack the farther one, so the
+// best t shrinks early and culls more of the tree; the result does not depend on the
+// order (lexicographic (t, index) minimum over every triangle whose box overlaps).
 template <bool ANY>
 __device__ bool bvh_trace(const KParams& P, uint32_t* stk, v3 o, v3 d, float tmax, float& bt, float& bu, float& bv,
                           int& bk) {
@@ -266,24 +279,22 @@ __device__ bool bvh_trace(const KParams& P, uint32_t* stk, v3 o, v3 d, float tma
         const f4 n0 = N[0], n1 = N[1], n2 = N[2], n3 = N[3];
         const float lim = ANY ? tmax : bt;
         const int lcount = __float_as_int(n1.w), rcount = __float_as_int(n3.w);
-        const bool hl = lcount >= 0 && bvh_box(n0, n1, o, inv, lim);
-        const bool hr = rcount >= 0 && bvh_box(n2, n3, o, inv, lim);
+        const float el = lcount >= 0 ? bvh_enter(n0, n1, o, inv, lim) : __builtin_inff();
+        const float er = rcount >= 0 ? bvh_enter(n2, n3, o, inv, lim) : __builtin_inff();
+        const bool hl = el != __builtin_inff(), hr = er != __builtin_inff();
+        // leaves first (either order gives the same result)
+        if (hl && lcount > 0 && bvh_leaf<ANY>(P, __float_as_int(n0.w), lcount, o, d, tmax, bt, bu, bv, bk)) return true;
+        if (hr && rcount > 0 && bvh_leaf<ANY>(P, __float_as_int(n2.w), rcount, o, d, tmax, bt, bu, bv, bk)) return true;
+        const bool il = hl && lcount == 0, ir = hr && rcount == 0;
         int next = -1;
-        if (hl) {
-            if (lcount > 0) {
-                if (bvh_leaf<ANY>(P, __float_as_int(n0.w), lcount, o, d, tmax, bt, bu, bv, bk)) return true;
-            } else {
-                next = __float_as_int(n0.w);
-            }
-        }
-        if (hr) {
-            if (rcount > 0) {
-                if (bvh_leaf<ANY>(P, __float_as_int(n2.w), rcount, o, d, tmax, bt, bu, bv, bk)) return true;
-            } else if (next < 0) {
-                next = __float_as_int(n2.w);
-            } else {
-                stk[(sp++) * kBlock] = (uint32_t)__float_as_int(n2.w);
-            }
+        if (il && ir) {
+            const bool lfirst = ANY || el <= er;
+            next = __float_as_int(lfirst ? n0.w : n2.w);
+            stk[(sp++) * kBlock] = (uint32_t)__float_as_int(lfirst ? n2.w : n0.w);
+        } else if (il) {
+            next = __float_as_int(n0.w);
+        } else if (ir) {
+            next = __float_as_int(n2.w);
         }
         if (next >= 0) {
             node = next;
@@ -298,7 +309,7 @@ __device__ bool bvh_trace(const KParams& P, uint32_t* stk, v3 o, v3 d, float tma
 template <int NL>
 __global__ __launch_bounds__(kBlock) void k_trace_bvh(KParams P, const uint32_t* __restrict__ list,
                                                        const uint32_t* __restrict__ count, uint32_t* zero_count) {
-    __shared__ uint32_t stack[kBvhMaxDepth * kBlock];
+    __shared__ uint32_t stack[kBvhStack * kBlock];
     zero_parts(P, zero_count);
     const PartIter it = part_iter(P, count, kBlock);
     const int tid = threadIdx.x;

@@ -315,7 +315,7 @@ int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
         const float diag = std::sqrt((hi[0] - lo[0]) * (hi[0] - lo[0]) + (hi[1] - lo[1]) * (hi[1] - lo[1]) +
                                      (hi[2] - lo[2]) * (hi[2] - lo[2]));
         const BvhBuild B = build_bvh(mn.data(), mx.data(), (uint32_t)nt, kBvhLeaf, 1e-4f * diag + 1e-4f, kBvhMaxDepth);
-        if (B.depth >= kBvhMaxDepth) return set_err(c, XRT_ERR_UNSUPPORTED, "BVH deeper than the traversal stack");
+        if (B.depth >= kBvhStack) return set_err(c, XRT_ERR_UNSUPPORTED, "BVH deeper than the traversal stack");
         std::vector<f4> btri(3 * nt);
         for (size_t i = 0; i < nt; ++i) {
             const uint32_t t = B.order[i];
