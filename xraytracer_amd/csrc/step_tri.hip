@@ -52,9 +52,13 @@ constexpr float kLambertPdfRcp = 1.0f / kLambertPdf;          // RN(1/pdf)
 
 // Stream words of one slot held in registers: b[0] is the next draw.  A segment draws at
 // most NW words (checked before it starts), so there is no fallback load.
+// The words of the next segment are prefetched into pf[] at the end of a segment and moved
+// into b[] only after the next trace (take), so the loads' latency hides behind the trace:
+// the move is the loads' first use, and nothing else in the loop reads pf[].
 template <int NW>
 struct RngRegs {
     uint32_t b[NW];
+    uint32_t pf[NW];
     uint32_t c;
     __device__ __forceinline__ void load(const uint32_t* ring) {
         gu32* r = glb<gu32>(ring);
@@ -64,6 +68,19 @@ struct RngRegs {
             b[j] = r[i];
             i = (i + 1 == kRing) ? 0u : i + 1;
         }
+    }
+    __device__ __forceinline__ void prefetch(const uint32_t* ring) {
+        gu32* r = glb<gu32>(ring);
+        uint32_t i = c % kRing;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+            pf[j] = r[i];
+            i = (i + 1 == kRing) ? 0u : i + 1;
+        }
+    }
+    __device__ __forceinline__ void take() {
+#pragma unroll
+        for (int j = 0; j < NW; ++j) b[j] = pf[j];
     }
     __device__ __forceinline__ float next() {
         const uint32_t y = b[0];
@@ -417,14 +434,18 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                 finish(rad_fin);
             }
         };
+        // a slot that starts a sample at the launch's first segment draws its jitter from
+        // the words loaded above; later segments start samples at their end (start_sample
+        // below), so no draw precedes the trace inside the loop
+        if (live && !(st & ST_DONE) && g - rng.c >= (uint32_t)NW && (st & ST_REGEN)) {
+            st &= ~ST_REGEN;
+            start_sample();
+        }
+        __builtin_amdgcn_s_waitcnt(0);   // prologue loads done: the loop waits only on its own prefetches
         MPH_DECL
         for (uint32_t vis = 0; vis < visits; ++vis) {
             const bool act = live && !(st & ST_DONE) && g - rng.c >= (uint32_t)NW;
             if (!__ballot(act || shm)) break;
-            if (act && (st & ST_REGEN)) {
-                st &= ~ST_REGEN;
-                start_sample();
-            }
             const bool ext_now = act && ext;
             MPH_MARK(0);
             unsigned long long best;
@@ -435,6 +456,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                 group_trace<NL, G>(P.n_objs, L, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
             MPH_MARK(1);
             resolve(occ);
+            if (vis > 0) rng.take();   // the words prefetched at the end of the previous segment
             MPH_MARK(2);
             if (ext_now) {
                 ++nseg;
@@ -548,7 +570,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                 }
             }
             MPH_MARK(3);
-            rng.load(ring);   // unconditional: the loads land straight in the loop-carried registers (no copy that would wait on them)
+            rng.prefetch(ring);   // unconditional; first read by take() after the next trace
 #ifdef XRT_PHASE_CLOCK
             ++ph_vis;
 #endif
