@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 4
+#define XRT_ABI_VERSION 5
 
 /* ---- status codes ---------------------------------------------------------------- */
 enum {
@@ -102,7 +102,13 @@ typedef struct {
 } xrt_medium_desc;
 
 /* ---- render parameters --------------------------------------------------------------- */
-enum { XRT_INTEGRATOR_GI = 0, XRT_INTEGRATOR_DIRECT = 1, XRT_INTEGRATOR_VPT = 2 };
+enum {
+    XRT_INTEGRATOR_GI = 0,        /* GIIntegrator(maxDepth)            Src/integrator.h:198-291 */
+    XRT_INTEGRATOR_DIRECT = 1,    /* DirectIntegrator                  Src/integrator.h:76-120  */
+    XRT_INTEGRATOR_VPT = 2,       /* VolumePathTracing(maxDepth)       Src/integrator.h:401-478 */
+    XRT_INTEGRATOR_INDIRECT = 3,  /* IndirectIntegrator(maxDepth)      Src/integrator.h:122-190 */
+    XRT_INTEGRATOR_NORMAL = 4     /* NormalIntegrator (shading normal) Src/integrator.h:22-74   */
+};
 enum {
     XRT_FLAG_TIMING = 1u,      /* time every kernel with HIP events (xrt_stats.kernel_ms)     */
     XRT_FLAG_WAVEFRONT = 2u,   /* force the multi-pass schedule (k_shade + k_trace) even when

@@ -1,13 +1,14 @@
-// xrt/integrator.h — the integrators of the benchmark configs (Src/integrator.h):
-// GIIntegrator (:198-291), DirectIntegrator (:76-120), VolumePathTracing (:401-478).
+// xrt/integrator.h — the reference's integrators (Src/integrator.h): GIIntegrator
+// (:198-291), DirectIntegrator (:76-120), VolumePathTracing (:401-478) — the benchmark
+// configs — and IndirectIntegrator (:122-190), NormalIntegrator (:22-74).
 // The host objects select the GPU pass schedule; they do not integrate on the CPU.
-// Normal/Indirect/Whitted/VPT-NEE are outside SURVEY.md §8 and not provided yet.
+// Whitted (delta lights) and VPT-NEE are not provided.
 #pragma once
 #include <cstdint>
 
 class Integrator {
 public:
-    enum class Kind { GI, Direct, VolumePathTracing };
+    enum class Kind { GI, Direct, VolumePathTracing, Indirect, Normal };
     explicit Integrator(Kind k, uint32_t maxDepth) : kind_(k), maxDepth_(maxDepth) {}
     virtual ~Integrator() = default;
     Kind kind() const { return kind_; }
@@ -31,4 +32,14 @@ public:
 class VolumePathTracing : public Integrator {
 public:
     explicit VolumePathTracing(uint32_t maxDepth) : Integrator(Kind::VolumePathTracing, maxDepth) {}
+};
+
+class IndirectIntegrator : public Integrator {
+public:
+    explicit IndirectIntegrator(int maxDepth) : Integrator(Kind::Indirect, (uint32_t)maxDepth) {}
+};
+
+class NormalIntegrator : public Integrator {
+public:
+    NormalIntegrator() : Integrator(Kind::Normal, 1) {}
 };

@@ -591,6 +591,62 @@ static v3 integrate_gi(const scene_ctx* C, v3 ro, v3 rd, uint32_t max_depth, orc
     return radiance;
 }
 
+/* IndirectIntegrator::integrate (Src/integrator.h:130-185): GIIntegrator's bounce loop with
+ * no light sampling; an area light adds throughput * Le at every depth */
+static v3 integrate_indirect(const scene_ctx* C, v3 ro, v3 rd, uint32_t max_depth, orc_mt* rng, path_counters* pc) {
+    const xrt_scene_desc* S = C->S;
+    v3 radiance = mk(0, 0, 0);
+    v3 thr = mk(1, 1, 1);
+    const v3 background = mk(0, 0, 0);
+    uint32_t depth = 0;
+    while (depth < max_depth) {
+        hinfo info;
+        hinfo_init(&info);
+        pc->segments++;
+        if (!scene_intersect(S, ro, rd, &info, &pc->tri_tests)) {
+            radiance = vadd(radiance, vmul(thr, background));
+            break;
+        }
+        if (depth > 0) {
+            const float p = smin((thr.x + thr.y + thr.z) / 3.0f, 1.0f);
+            if (orc_draw(rng) >= p) break;
+            thr = vdivv(thr, mk(p, p, p));
+        }
+        const xrt_object* ob = &S->objects[info.hit];
+        if (ob->light >= 0) {
+            radiance = vadd(radiance, vmul(thr, light_Le(&S->lights[ob->light], info.ns, rd)));
+            break;
+        }
+        float pdf = 1.0f;
+        v3 nextDir = mk(0, 0, 0);
+        v3 fr = mk(0, 0, 0);
+        if (ob->material == XRT_MAT_LAMBERT) {
+            nextDir = lambert_sample_dir(info.ng, info.dpdu, info.dpdv, rng, &pdf);
+            fr = eval_bxdf(ob);
+        }
+        float cosv = smax(.0f, vdot(nextDir, info.ng));
+        const float bias = 0.01f;
+        thr = vmul(thr, vdivs(vmuls(fr, cosv), pdf));
+        ro = vadd(info.pos, vmuls(info.ng, bias));
+        rd = nextDir;
+        depth++;
+    }
+    return radiance;
+}
+
+/* NormalIntegrator::integrate (Src/integrator.h:28-37): 0.5 * (ns + 1) on a hit, else 0.
+ * (Everything after its first return is unreachable.) */
+static v3 integrate_normal(const scene_ctx* C, v3 ro, v3 rd, path_counters* pc) {
+    hinfo info;
+    hinfo_init(&info);
+    pc->segments++;
+    if (scene_intersect(C->S, ro, rd, &info, &pc->tri_tests)) {
+        const v3 a = mk(info.ns.x + 1.0f, info.ns.y + 1.0f, info.ns.z + 1.0f);
+        return mk(0.5f * a.x, 0.5f * a.y, 0.5f * a.z);
+    }
+    return mk(0, 0, 0);
+}
+
 /* DirectIntegrator::integrate (Src/integrator.h:82-119) */
 static v3 integrate_direct(const scene_ctx* C, v3 ro, v3 rd, orc_mt* rng, path_counters* pc) {
     const xrt_scene_desc* S = C->S;
@@ -690,6 +746,8 @@ static void camera_ray(const orc_camera* cam, float u, float v, v3* o, v3* d) {
 static v3 integrate(const scene_ctx* C, const xrt_render_params* p, v3 ro, v3 rd, orc_mt* rng, path_counters* pc) {
     if (p->integrator == XRT_INTEGRATOR_DIRECT) return integrate_direct(C, ro, rd, rng, pc);
     if (p->integrator == XRT_INTEGRATOR_VPT) return integrate_vpt(C, ro, rd, p->max_depth, rng, pc);
+    if (p->integrator == XRT_INTEGRATOR_INDIRECT) return integrate_indirect(C, ro, rd, p->max_depth, rng, pc);
+    if (p->integrator == XRT_INTEGRATOR_NORMAL) return integrate_normal(C, ro, rd, pc);
     return integrate_gi(C, ro, rd, p->max_depth, rng, pc);
 }
 

@@ -291,6 +291,25 @@ def test_sphere_bvh_ties_and_gi(renderer, sched, integ):
     assert renderer.stats.shadow_rays == st["shadow_rays"]
 
 
+@pytest.mark.parametrize("integ,depth", [("indirect", 3), ("indirect", 5), ("normal", 1)])
+def test_indirect_and_normal_integrators(renderer, sched, integ, depth):
+    """IndirectIntegrator (Src/integrator.h:122-190) and NormalIntegrator (:22-74) on the
+    Cornell box (triangles) and the sphere scene, bit-exact against the oracle."""
+    for s, w, h in ((scenes.cornell(64, 48), 64, 48), (dup_spheres(48, 36), 48, 36)):
+        img, ref, st = render_both(renderer, s, w, h, 4, integrator=integ, max_depth=depth, schedule=sched)
+        compare(img, ref)
+        assert renderer.stats.segments == st["segments"]
+        assert renderer.stats.draws == st["draws"]
+
+
+def test_normal_integrator_on_medium_box(renderer, sched):
+    """NormalIntegrator over the smoke scene: a BoxMesh hit leaves the shading normal at its
+    default (0), so the pixel is 0.5 — as in the reference."""
+    s = scenes.smoke(32, 24)
+    img, ref, _ = render_both(renderer, s, 32, 24, 2, integrator="normal", schedule=sched)
+    compare(img, ref)
+
+
 @pytest.mark.parametrize("nt,w,h,spp", [(24, 64, 36, 4), (80, 48, 30, 3)])
 def test_c4_sphere_mesh_gi(renderer, nt, w, h, spp):
     """Config C4 scene family (Cornell + tessellated sphere; 1,152 and 12,800 mesh triangles)

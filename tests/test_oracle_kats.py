@@ -144,3 +144,22 @@ def test_path_counters_match_reference_probe():
     assert round(st["shadow_rays"] / n, 3) in (0.751, 0.752)
     assert round(st["tri_tests"] / n, 1) == 84.5
     assert st["rejected"] == 0
+
+
+def test_indirect_and_normal_integrators_oracle():
+    """CPU restatements of IndirectIntegrator / NormalIntegrator (parity unpinned beyond the
+    building-block KATs; the GPU parity tests compare against these): NormalIntegrator draws
+    only the two jitter words per sample and returns 0.5 * (ns + 1) (or 0 on a miss);
+    IndirectIntegrator never samples lights."""
+    import numpy as np
+    from xraytracer_amd import scenes
+
+    s = scenes.cornell(32, 24)
+    img, st = pyoracle.render(s, 32, 24, 4, integrator="normal")
+    assert st["draws"] == 2 * st["samples"] and st["shadow_rays"] == 0
+    assert np.all(img >= 0.0) and np.all(img <= 1.0)
+    assert np.any(img == 0.0) and np.any(img > 0.4)
+    img, st = pyoracle.render(s, 32, 24, 4, integrator="indirect", max_depth=3)
+    assert st["shadow_rays"] == 0 and np.all(np.isfinite(img)) and img.max() > 0
+    gi, stg = pyoracle.render(s, 32, 24, 4, integrator="gi", max_depth=3)
+    assert stg["shadow_rays"] > 0 and not np.array_equal(img, gi)

@@ -16,19 +16,21 @@ LIB_PATH = os.path.join(HERE, "libxrt_hip.so")
 if os.environ.get("XRT_LIB"):   # experiment builds (csrc/Makefile `variant`), same ABI
     LIB_PATH = os.path.join(HERE, os.environ["XRT_LIB"])
 
-XRT_ABI_VERSION = 4   # include/xrt.h XRT_ABI_VERSION
+XRT_ABI_VERSION = 5   # include/xrt.h XRT_ABI_VERSION
 XRT_OK = 0
 XRT_OBJ_MESH, XRT_OBJ_SPHERE, XRT_OBJ_BOX = 0, 1, 2
 XRT_LIGHT_QUAD, XRT_LIGHT_TRIANGLE, XRT_LIGHT_SPHERE = 0, 1, 2
 XRT_MAT_NONE, XRT_MAT_LAMBERT = 0, 1
 XRT_INTEGRATOR_GI, XRT_INTEGRATOR_DIRECT, XRT_INTEGRATOR_VPT = 0, 1, 2
+XRT_INTEGRATOR_INDIRECT, XRT_INTEGRATOR_NORMAL = 3, 4
 XRT_FLAG_TIMING, XRT_FLAG_WAVEFRONT, XRT_FLAG_NO_MERGED = 1, 2, 4
 XRT_SCHED_WAVEFRONT, XRT_SCHED_STEP, XRT_SCHED_STEP_TRI, XRT_SCHED_STEP_MERGED = 0, 1, 2, 3
 SCHEDULE_NAMES = ("wavefront", "step", "step_tri", "step_merged")
 XRT_K_SEED, XRT_K_TRACE, XRT_K_SHADE, XRT_K_FINISH, XRT_K_STEP, XRT_K_REFILL, XRT_K_COUNT = 0, 1, 2, 3, 4, 5, 6
 KERNEL_NAMES = ("seed", "trace", "shade", "finish", "step", "refill")
 
-INTEGRATORS = {"gi": XRT_INTEGRATOR_GI, "direct": XRT_INTEGRATOR_DIRECT, "vpt": XRT_INTEGRATOR_VPT}
+INTEGRATORS = {"gi": XRT_INTEGRATOR_GI, "direct": XRT_INTEGRATOR_DIRECT, "vpt": XRT_INTEGRATOR_VPT,
+               "indirect": XRT_INTEGRATOR_INDIRECT, "normal": XRT_INTEGRATOR_NORMAL}
 
 f32p = C.POINTER(C.c_float)
 u32p = C.POINTER(C.c_uint32)

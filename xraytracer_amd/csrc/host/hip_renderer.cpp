@@ -44,6 +44,8 @@ void HipRenderer::render(const Scene& scene, Sampler::SamplerType, Image& image)
         case Integrator::Kind::GI: p.integrator = XRT_INTEGRATOR_GI; break;
         case Integrator::Kind::Direct: p.integrator = XRT_INTEGRATOR_DIRECT; break;
         case Integrator::Kind::VolumePathTracing: p.integrator = XRT_INTEGRATOR_VPT; break;
+        case Integrator::Kind::Indirect: p.integrator = XRT_INTEGRATOR_INDIRECT; break;
+        case Integrator::Kind::Normal: p.integrator = XRT_INTEGRATOR_NORMAL; break;
     }
     if (p.integrator == XRT_INTEGRATOR_VPT) {
         const HeterogeneousMedium* med = scene.medium();

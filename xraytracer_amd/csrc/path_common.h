@@ -397,6 +397,12 @@ __host__ __device__ inline StepLayout step_layout(const KParams& P) {
     return L;
 }
 
+// NormalIntegrator's colour 0.5f * (ns + 1.0f) (Src/integrator.h:36): Vec3f + float, then
+// float * Vec3f, component-wise
+__device__ __forceinline__ v3 normal_color(v3 ns) {
+    return mk(0.5f * (ns.x + 1.0f), 0.5f * (ns.y + 1.0f), 0.5f * (ns.z + 1.0f));
+}
+
 // ============================================================ fused schedule ====
 // k_step: per live slot, up to `visits` path segments in one launch with the path state in
 // registers: trace the pending ray, shade the hit (NEE shadow rays traced immediately, so

@@ -14,6 +14,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "xrt.h"
+
 #ifndef __HIPCC__
 struct float4_ { float x, y, z, w; };
 #endif
@@ -53,6 +55,9 @@ enum : uint32_t {
 
 enum : int { SEG_TRI = 0, SEG_SPHERE = 1, SEG_BOX = 2 };
 enum : int { SCN_TRI = 0, SCN_SPHERE = 1, SCN_MIXED = 2 };  // trace kernel specialisations
+// integrators that trace exactly one ray per sample (Direct, Normal): no bounce loop, so
+// maxDepth 0 does not zero their samples
+constexpr bool one_hit(int integ) { return integ == XRT_INTEGRATOR_DIRECT || integ == XRT_INTEGRATOR_NORMAL; }
 
 struct DSeg {   // a run of consecutive objects of one kind, in iteration order
     int kind, first, count, pad;

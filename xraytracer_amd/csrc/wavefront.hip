@@ -705,8 +705,14 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
                         if (smask) st |= ST_NEE | ST_END | (smask << ST_SHADOW_SHIFT);
                         else finalize = true;
                     }
+                } else if (INTEG == XRT_INTEGRATOR_NORMAL) {
+                    // NormalIntegrator::integrate (Src/integrator.h:28-37): 0.5 * (ns + 1)
+                    if (obj >= 0) rad = normal_color(S.ns);
+                    finalize = true;
                 } else {
-                    // GIIntegrator::integrate loop body (Src/integrator.h:214-284)
+                    // GIIntegrator::integrate loop body (Src/integrator.h:214-284);
+                    // IndirectIntegrator (Src/integrator.h:138-185): no light sampling, Le at
+                    // every depth
                     if (obj < 0) {
                         rad = rad + thr * mk(0.0f, 0.0f, 0.0f);
                         finalize = true;
@@ -719,12 +725,13 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
                         }
                         const DObj ob = P.objs[obj];
                         if (alive && ob.light >= 0) {
-                            if (depth == 0) rad = rad + thr * light_Le(P.lights[ob.light], S.ns, d);
+                            if (depth == 0 || INTEG == XRT_INTEGRATOR_INDIRECT)
+                                rad = rad + thr * light_Le(P.lights[ob.light], S.ns, d);
                             alive = false, finalize = true;
                         }
                         if (alive) {
                             uint32_t smask = 0;
-                            for (int l = 0; l < P.n_lights; ++l) {
+                            for (int l = 0; l < (INTEG == XRT_INTEGRATOR_GI ? P.n_lights : 0); ++l) {
                                 v3 wi = mk(0, 0, 0);
                                 float tmax = 0.0f, pdf = 0.0f;
                                 const v3 L = light_sample(P.lights[l], S.pos, wi, pdf, tmax, rng);
@@ -741,7 +748,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
                             if (smask) {
                                 P.thr_prev[s] = pk(thr);
                                 st |= ST_NEE | (smask << ST_SHADOW_SHIFT);
-                            } else {
+                            } else if (INTEG == XRT_INTEGRATOR_GI) {
                                 rad = rad + thr * mk(0, 0, 0);   // radiance += thr * directL(=0)
                             }
                             // indirect: Object::sampleBxDF -> Lambert (no material: 0, no draws)
@@ -802,7 +809,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
                 thr = mk(1, 1, 1);
                 rad = mk(0, 0, 0);
                 depth = 0;
-                if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) {
+                if (!one_hit(INTEG) && P.max_depth == 0) {
                     finalize = true;   // the bounce loop never runs: radiance 0
                     continue;
                 }
@@ -819,7 +826,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
                 thr = mk(1, 1, 1);
                 rad = mk(0, 0, 0);
                 depth = 0;
-                if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) {
+                if (!one_hit(INTEG) && P.max_depth == 0) {
                     // degenerate: every sample is 0 — finish all of them here
                     while (true) {
                         ++k;
@@ -1157,7 +1164,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
                 camera_ray(P, u, v, o, d);
                 thr = mk(1, 1, 1), rad = mk(0, 0, 0);
                 depth = 0;
-                if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) ended = true, trace = false;
+                if (!one_hit(INTEG) && P.max_depth == 0) ended = true, trace = false;
             } else if (INTEG == XRT_INTEGRATOR_VPT && (st & ST_MEDIUM)) {
                 trace = false;
             }
@@ -1226,8 +1233,14 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
                             }
                         }
                     }
+                } else if (INTEG == XRT_INTEGRATOR_NORMAL) {
+                    // NormalIntegrator::integrate (Src/integrator.h:28-37): 0.5 * (ns + 1)
+                    if (obj >= 0) rad = normal_color(S.ns);
+                    ended = true;
                 } else {
-                    // GIIntegrator::integrate loop body (Src/integrator.h:214-284)
+                    // GIIntegrator::integrate loop body (Src/integrator.h:214-284);
+                    // IndirectIntegrator (Src/integrator.h:138-185): no light sampling, Le at
+                    // every depth
                     if (obj < 0) {
                         rad = rad + thr * mk(0.0f, 0.0f, 0.0f);
                         ended = true;
@@ -1240,12 +1253,13 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
                         }
                         const DObj& ob = L.obj[obj];
                         if (alive && ob.light >= 0) {
-                            if (depth == 0) rad = rad + thr * light_Le(L.light[ob.light], S.ns, d);
+                            if (depth == 0 || INTEG == XRT_INTEGRATOR_INDIRECT)
+                                rad = rad + thr * light_Le(L.light[ob.light], S.ns, d);
                             alive = false, ended = true;
                         }
                         if (alive) {
                             v3 directL = mk(0, 0, 0);
-                            for (int l = 0; l < P.n_lights; ++l) {
+                            for (int l = 0; l < (INTEG == XRT_INTEGRATOR_GI ? P.n_lights : 0); ++l) {
                                 v3 L_light = mk(0, 0, 0);
                                 v3 wi = mk(0, 0, 0);
                                 float tmax = 0.0f, pdf = 0.0f;
@@ -1259,7 +1273,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
                                 L_light = L_light + (((fr * (float)vis) * Lv) * cosv) / pdf;
                                 directL = directL + L_light;
                             }
-                            rad = rad + thr * directL;
+                            if (INTEG == XRT_INTEGRATOR_GI) rad = rad + thr * directL;
                             float pdf = 1.0f;
                             v3 nd = mk(0, 0, 0), fr = mk(0, 0, 0);
                             if (ob.material == 1) {
@@ -1307,7 +1321,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
                 ++k;
                 if (k >= P.spp) {
                     st = ST_DONE;
-                } else if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) {
+                } else if (!one_hit(INTEG) && P.max_depth == 0) {
                     (void)rng.next(), (void)rng.next();   // the next sample's jitter; radiance 0
                     rad = mk(0, 0, 0);
                     ended = true;
@@ -1557,7 +1571,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
                 depth = 0;
             }
             bool ended = false, alive = false;
-            if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) ended = act;   // bounce loop never runs
+            if (!one_hit(INTEG) && P.max_depth == 0) ended = act;   // bounce loop never runs
             const bool ext = act && !ended;
             HitRec h;
             PH_MARK(0);
@@ -1671,7 +1685,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
                 ++k;
                 if (k >= P.spp) {
                     st = ST_DONE;
-                } else if (INTEG != XRT_INTEGRATOR_DIRECT && P.max_depth == 0) {
+                } else if (!one_hit(INTEG) && P.max_depth == 0) {
                     (void)rng.next(), (void)rng.next();
                     rad = mk(0, 0, 0);
                     ended = true;
@@ -1921,6 +1935,12 @@ static hipError_t shade_i(const KParams& P, const uint32_t* list, const uint32_t
     else if (P.integrator == XRT_INTEGRATOR_VPT)
         hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_VPT>), dim3(blocks), dim3(kBlock), 0, st, P, list, count,
                            out, out_count, req_count);
+    else if (P.integrator == XRT_INTEGRATOR_INDIRECT)
+        hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_INDIRECT>), dim3(blocks), dim3(kBlock), 0, st, P, list, count,
+                           out, out_count, req_count);
+    else if (P.integrator == XRT_INTEGRATOR_NORMAL)
+        hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_NORMAL>), dim3(blocks), dim3(kBlock), 0, st, P, list, count,
+                           out, out_count, req_count);
     else
         hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_GI>), dim3(blocks), dim3(kBlock), 0, st, P, list, count,
                            out, out_count, req_count);
@@ -1954,6 +1974,12 @@ static hipError_t step_i(const KParams& P, const uint32_t* list, const uint32_t*
     else if (P.integrator == XRT_INTEGRATOR_VPT)
         hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_VPT>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
                            out, out_count, zero, req_count, visits);
+    else if (P.integrator == XRT_INTEGRATOR_INDIRECT)
+        hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_INDIRECT>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
+                           out, out_count, zero, req_count, visits);
+    else if (P.integrator == XRT_INTEGRATOR_NORMAL)
+        hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_NORMAL>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
+                           out, out_count, zero, req_count, visits);
     else
         hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_GI>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
                            out, out_count, zero, req_count, visits);
@@ -1962,7 +1988,7 @@ static hipError_t step_i(const KParams& P, const uint32_t* list, const uint32_t*
 
 bool use_step_tri(const KParams& P) {
     return P.scene_kind == SCN_TRI && P.small_tri && P.n_objs <= kCoopMaxObjs &&
-           P.integrator != XRT_INTEGRATOR_VPT && !std::getenv("XRT_NO_COOP") &&
+           (P.integrator == XRT_INTEGRATOR_GI || P.integrator == XRT_INTEGRATOR_DIRECT) && !std::getenv("XRT_NO_COOP") &&
            ((step_layout(P).total + 15u) & ~15u) + (kBlock / 64) * sizeof(CoopWave) <= kStepLds;
 }
 

@@ -408,8 +408,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     if (!c->has_scene || !c->has_camera) return set_err(c, XRT_ERR_STATE, "upload a scene and set a camera first");
     if (p->width == 0 || p->height == 0 || p->shard_count == 0 || p->shard_index >= p->shard_count)
         return set_err(c, XRT_ERR_INVALID, "bad image size or shard");
-    if (p->integrator != XRT_INTEGRATOR_GI && p->integrator != XRT_INTEGRATOR_DIRECT &&
-        p->integrator != XRT_INTEGRATOR_VPT)
+    if (p->integrator < XRT_INTEGRATOR_GI || p->integrator > XRT_INTEGRATOR_NORMAL)
         return set_err(c, XRT_ERR_INVALID, "unknown integrator");
     if (p->integrator == XRT_INTEGRATOR_VPT && !c->has_medium)
         return set_err(c, XRT_ERR_STATE, "VolumePathTracing needs xrt_set_medium first");
