@@ -107,7 +107,8 @@ enum {
     XRT_INTEGRATOR_DIRECT = 1,    /* DirectIntegrator                  Src/integrator.h:76-120  */
     XRT_INTEGRATOR_VPT = 2,       /* VolumePathTracing(maxDepth)       Src/integrator.h:401-478 */
     XRT_INTEGRATOR_INDIRECT = 3,  /* IndirectIntegrator(maxDepth)      Src/integrator.h:122-190 */
-    XRT_INTEGRATOR_NORMAL = 4     /* NormalIntegrator (shading normal) Src/integrator.h:22-74   */
+    XRT_INTEGRATOR_NORMAL = 4,    /* NormalIntegrator (shading normal) Src/integrator.h:22-74   */
+    XRT_INTEGRATOR_VPT_NEE = 5    /* VolumePathTracingNEE(maxDepth)    Src/integrator.h:481-636 */
 };
 enum {
     XRT_FLAG_TIMING = 1u,      /* time every kernel with HIP events (xrt_stats.kernel_ms)     */

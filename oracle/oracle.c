@@ -717,6 +717,100 @@ static v3 integrate_vpt(const scene_ctx* C, v3 ro, v3 rd, uint32_t max_depth, or
     return radiance;
 }
 
+/* HeterogeneousMedium::ratioTrackingTransmittance (Src/medium.h:360-386) */
+static v3 ratio_tracking(const scene_ctx* C, v3 p1, v3 p2, orc_mt* rng) {
+    const xrt_medium_desc* M = C->M;
+    const float majorant = C->majorant, invMajorant = C->inv_majorant;
+    const v3 vmaj = mk(majorant, majorant, majorant);
+    const float distToEnd = vlength(vsub(p1, p2));
+    float t = 0;
+    const v3 dn = vnormalize(vsub(p2, p1));
+    v3 tr = mk(1, 1, 1);
+    for (;;) {
+        const float s = -logf(smax(1.0f - orc_draw(rng), 0.0f)) * invMajorant;
+        t += s;
+        if (t > distToEnd) break;
+        const float density = medium_density(M, ray_at(p1, dn, t));
+        const v3 sigma_n = vsub(vsub(vmaj, vmuls(ld3(M->absorption), density)), vmuls(ld3(M->scattering), density));
+        tr = vmul(tr, vmuls(sigma_n, invMajorant));
+    }
+    return tr;
+}
+
+/* VolumePathTracingNEE::integrate (Src/integrator.h:489-584) with sampleDirectionToLight
+ * (:586-602, Scene::sampleAreaLight Src/scene.cpp:182-188) and isVisible (:604-631):
+ * the shadow ray takes the closest hit, a surface occludes, a medium attenuates by ratio
+ * tracking between the hit's t and t1.  Objects with neither light nor medium stall the
+ * path as in integrate_vpt. */
+static v3 integrate_vpt_nee(const scene_ctx* C, v3 ro, v3 rd, uint32_t max_depth, orc_mt* rng, path_counters* pc) {
+    const xrt_scene_desc* S = C->S;
+    v3 radiance = mk(0, 0, 0);
+    v3 thr = mk(1, 1, 1);
+    const v3 background = mk(0.0f, 0.0f, 0.0f);
+    uint32_t depth = 0;
+    while (depth < max_depth) {
+        hinfo info;
+        hinfo_init(&info);
+        pc->segments++;
+        if (!scene_intersect(S, ro, rd, &info, &pc->tri_tests)) {
+            radiance = vadd(radiance, vmuls(vmul(thr, background), (float)(depth != 0)));
+            break;
+        }
+        if (depth > 0) {
+            const float p = smin((thr.x + thr.y + thr.z) / 3.0f, 1.0f);
+            if (orc_draw(rng) >= p) break;
+            thr = vdivv(thr, mk(p, p, p));
+        }
+        const xrt_object* ob = &S->objects[info.hit];
+        if (ob->light >= 0) {
+            if (depth == 0) radiance = vadd(radiance, vmul(thr, light_Le(&S->lights[ob->light], info.ns, rd)));
+            break;
+        }
+        if (ob->medium >= 0 && C->M) {
+            v3 pos, dir, tm;
+            const int scattered = sample_medium(C, ro, rd, thr, &info, rng, &pos, &dir, &tm, &pc->ub_channel);
+            if (scattered) {
+                /* light index: (unsigned)(size * u), clamped; pdf 1 / size */
+                unsigned li = (unsigned)((float)S->n_lights * orc_draw(rng));
+                if (li == S->n_lights) li--;
+                const float choose = 1.0f / (float)S->n_lights;
+                v3 wl = mk(0, 0, 0);
+                float lpdf = 0.0f, dist = 0.0f;
+                const v3 Le = light_sample(&S->lights[li], pos, &wl, &lpdf, &dist, rng);
+                const float pdf_dir = choose * lpdf;
+                if (pdf_dir > 0.0f) {
+                    v3 transmittance = mk(1, 1, 1);
+                    int visible = 1;
+                    hinfo sh;
+                    hinfo_init(&sh);
+                    pc->shadow_rays++;
+                    if (scene_intersect(S, pos, wl, &sh, &pc->tri_tests)) {
+                        const xrt_object* so = &S->objects[sh.hit];
+                        if (so->material != XRT_MAT_NONE) {
+                            visible = 0;
+                        } else if (so->medium >= 0) {
+                            transmittance = vmul(transmittance, ratio_tracking(C, ray_at(pos, wl, sh.t), ray_at(pos, wl, sh.t1), rng));
+                        }
+                    }
+                    if (visible) {
+                        const float f = hg_evaluate(C->M->g, rd, wl);
+                        const v3 Ls = vdivs(vmul(vmuls(transmittance, f), Le), pdf_dir);
+                        radiance = vadd(radiance, vmul(vmul(thr, tm), Ls));
+                    }
+                }
+            }
+            ro = pos;
+            rd = dir;
+            thr = vmul(thr, tm);
+            if (scattered) depth++;
+        } else {
+            pc->stalled++;
+            break;
+        }
+    }
+    return radiance;
+}
+
 /* ---------------------------------------------------------------- renderer ---- */
 static int setup_ctx(scene_ctx* C, const xrt_scene_desc* S, const xrt_medium_desc* M) {
     C->S = S;
@@ -748,6 +842,7 @@ static v3 integrate(const scene_ctx* C, const xrt_render_params* p, v3 ro, v3 rd
     if (p->integrator == XRT_INTEGRATOR_VPT) return integrate_vpt(C, ro, rd, p->max_depth, rng, pc);
     if (p->integrator == XRT_INTEGRATOR_INDIRECT) return integrate_indirect(C, ro, rd, p->max_depth, rng, pc);
     if (p->integrator == XRT_INTEGRATOR_NORMAL) return integrate_normal(C, ro, rd, pc);
+    if (p->integrator == XRT_INTEGRATOR_VPT_NEE) return integrate_vpt_nee(C, ro, rd, p->max_depth, rng, pc);
     return integrate_gi(C, ro, rd, p->max_depth, rng, pc);
 }
 
@@ -784,7 +879,7 @@ static v3 do_render_pixel(const scene_ctx* C, const orc_camera* cam, const xrt_r
 
 static int check_params(const xrt_scene_desc* S, const xrt_render_params* p, const xrt_medium_desc* M) {
     if (!S || !p || p->width == 0 || p->height == 0 || p->shard_count == 0 || p->shard_index >= p->shard_count) return -1;
-    if (p->integrator == XRT_INTEGRATOR_VPT && !M) return -1;
+    if ((p->integrator == XRT_INTEGRATOR_VPT || p->integrator == XRT_INTEGRATOR_VPT_NEE) && !M) return -1;
     return 0;
 }
 

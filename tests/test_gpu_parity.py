@@ -357,6 +357,43 @@ def test_vpt_medium_walk_suspends_and_resumes(renderer, sched):
     assert renderer.stats.draws == st["draws"]
 
 
+def dense_smoke(w, h, n=24, g=0.4):
+    """Smoke scene with a denser, anisotropic medium: more scattering events, more NEE ratio
+    tracking steps per light sample, HenyeyGreenstein with g != 0."""
+    s = scenes.SceneBundle()
+    med = scenes.Medium(scenes.smoke_grid(n, seed=3), (0.0, 0.0, 0.0), 1.0, g, (0.05, 0.02, 0.01), (0.4, 0.5, 0.6),
+                        multiplier=1.5)
+    c = (n - 1) / 2.0
+    s.add_quad_light("QuadLight", (c + 10, n + 15.0, c + 10), (c - 10, n + 15.0, c + 10), (c + 10, n + 15.0, c - 10),
+                     (20.0, 20.0, 20.0))
+    s.add_medium("medium", med)
+    s.flatten()
+    s.camera = scenes.pinhole((1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, c, c, c + 2.2 * n, 1), 45.0, w, h)
+    s.integrator, s.max_depth = "vpt_nee", 10
+    return s
+
+
+@pytest.mark.parametrize("dense", [False, True])
+def test_vpt_nee(renderer, sched, dense):
+    """VolumePathTracingNEE (Src/integrator.h:481-636): light sample at every scattering
+    event, shadow ray's closest hit, ratio-tracking transmittance through the medium."""
+    s = dense_smoke(40, 30) if dense else scenes.smoke(40, 30, n=32)
+    img, ref, st = render_both(renderer, s, 40, 30, 4, integrator="vpt_nee", schedule=sched)
+    compare(img, ref)
+    g = renderer.stats
+    assert g.draws == st["draws"] and g.segments == st["segments"] and g.shadow_rays == st["shadow_rays"]
+    assert st["shadow_rays"] > 0
+
+
+def test_vpt_nee_ratio_tracking_suspends_and_resumes(renderer, sched):
+    """Many spp on a few pixels of the dense medium: NEE ratio tracking (and delta tracking)
+    runs out of RNG words mid-walk and resumes after the refill."""
+    s = dense_smoke(8, 6)
+    img, ref, st = render_both(renderer, s, 8, 6, 160, integrator="vpt_nee", schedule=sched)
+    compare(img, ref)
+    assert renderer.stats.draws == st["draws"]
+
+
 @pytest.mark.parametrize("kind", ["gi", "direct"])
 def test_cpp_api_example_matches_oracle(tmp_path, kind):
     """examples/cornellbox.cpp — the reference example written against include/xrt/*.h with

@@ -163,3 +163,19 @@ def test_indirect_and_normal_integrators_oracle():
     assert st["shadow_rays"] == 0 and np.all(np.isfinite(img)) and img.max() > 0
     gi, stg = pyoracle.render(s, 32, 24, 4, integrator="gi", max_depth=3)
     assert stg["shadow_rays"] > 0 and not np.array_equal(img, gi)
+
+
+def test_vpt_nee_oracle():
+    """CPU restatement of VolumePathTracingNEE (parity unpinned beyond the building-block
+    KATs — HenyeyGreenstein, sampleWavelength, BoxMesh — and the glibc logf/expf it calls):
+    light samples happen only at scattering events, so there are fewer shadow rays than
+    segments, and the image is finite and non-negative."""
+    import numpy as np
+    from xraytracer_amd import scenes
+
+    s = scenes.smoke(24, 18, n=24)
+    img, st = pyoracle.render(s, 24, 18, 4, integrator="vpt_nee")
+    assert 0 < st["shadow_rays"] < st["segments"] and st["stalled"] == 0
+    assert np.all(np.isfinite(img)) and np.all(img >= 0) and img.max() > 0
+    vpt, stv = pyoracle.render(s, 24, 18, 4, integrator="vpt")
+    assert stv["shadow_rays"] == 0 and not np.array_equal(img, vpt)

@@ -22,7 +22,7 @@ XRT_OBJ_MESH, XRT_OBJ_SPHERE, XRT_OBJ_BOX = 0, 1, 2
 XRT_LIGHT_QUAD, XRT_LIGHT_TRIANGLE, XRT_LIGHT_SPHERE = 0, 1, 2
 XRT_MAT_NONE, XRT_MAT_LAMBERT = 0, 1
 XRT_INTEGRATOR_GI, XRT_INTEGRATOR_DIRECT, XRT_INTEGRATOR_VPT = 0, 1, 2
-XRT_INTEGRATOR_INDIRECT, XRT_INTEGRATOR_NORMAL = 3, 4
+XRT_INTEGRATOR_INDIRECT, XRT_INTEGRATOR_NORMAL, XRT_INTEGRATOR_VPT_NEE = 3, 4, 5
 XRT_FLAG_TIMING, XRT_FLAG_WAVEFRONT, XRT_FLAG_NO_MERGED = 1, 2, 4
 XRT_SCHED_WAVEFRONT, XRT_SCHED_STEP, XRT_SCHED_STEP_TRI, XRT_SCHED_STEP_MERGED = 0, 1, 2, 3
 SCHEDULE_NAMES = ("wavefront", "step", "step_tri", "step_merged")
@@ -30,7 +30,7 @@ XRT_K_SEED, XRT_K_TRACE, XRT_K_SHADE, XRT_K_FINISH, XRT_K_STEP, XRT_K_REFILL, XR
 KERNEL_NAMES = ("seed", "trace", "shade", "finish", "step", "refill")
 
 INTEGRATORS = {"gi": XRT_INTEGRATOR_GI, "direct": XRT_INTEGRATOR_DIRECT, "vpt": XRT_INTEGRATOR_VPT,
-               "indirect": XRT_INTEGRATOR_INDIRECT, "normal": XRT_INTEGRATOR_NORMAL}
+               "indirect": XRT_INTEGRATOR_INDIRECT, "normal": XRT_INTEGRATOR_NORMAL, "vpt_nee": XRT_INTEGRATOR_VPT_NEE}
 
 f32p = C.POINTER(C.c_float)
 u32p = C.POINTER(C.c_uint32)

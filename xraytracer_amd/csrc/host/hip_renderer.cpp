@@ -46,8 +46,9 @@ void HipRenderer::render(const Scene& scene, Sampler::SamplerType, Image& image)
         case Integrator::Kind::VolumePathTracing: p.integrator = XRT_INTEGRATOR_VPT; break;
         case Integrator::Kind::Indirect: p.integrator = XRT_INTEGRATOR_INDIRECT; break;
         case Integrator::Kind::Normal: p.integrator = XRT_INTEGRATOR_NORMAL; break;
+        case Integrator::Kind::VolumePathTracingNEE: p.integrator = XRT_INTEGRATOR_VPT_NEE; break;
     }
-    if (p.integrator == XRT_INTEGRATOR_VPT) {
+    if (p.integrator == XRT_INTEGRATOR_VPT || p.integrator == XRT_INTEGRATOR_VPT_NEE) {
         const HeterogeneousMedium* med = scene.medium();
         const DenseGrid* grid = med ? dynamic_cast<const DenseGrid*>(med->grid()) : nullptr;
         if (!grid) return fail(XRT_ERR_UNSUPPORTED, "VolumePathTracing needs a HeterogeneousMedium over a DenseGrid");

@@ -50,6 +50,7 @@ enum : uint32_t {
     ST_DONE = 16u,    // all samples of this pixel are done
     ST_MEDIUM = 32u,  // VPT delta-tracking loop suspended (resumes after an RNG refill)
     ST_RNGREQ = 64u,  // slot is on the refill list (k_refill twists its ring and clears this)
+    ST_NEEWALK = 128u,// VPT-NEE: the light sample's ratio tracking is suspended (state in KParams::nee)
     ST_SHADOW_SHIFT = 8u  // bits 8..15: which lights have a shadow ray in flight
 };
 
@@ -58,6 +59,8 @@ enum : int { SCN_TRI = 0, SCN_SPHERE = 1, SCN_MIXED = 2 };  // trace kernel spec
 // integrators that trace exactly one ray per sample (Direct, Normal): no bounce loop, so
 // maxDepth 0 does not zero their samples
 constexpr bool one_hit(int integ) { return integ == XRT_INTEGRATOR_DIRECT || integ == XRT_INTEGRATOR_NORMAL; }
+// volumetric integrators (VolumePathTracing and its NEE variant): delta tracking through media
+constexpr bool vpt_family(int integ) { return integ == XRT_INTEGRATOR_VPT || integ == XRT_INTEGRATOR_VPT_NEE; }
 
 struct DSeg {   // a run of consecutive objects of one kind, in iteration order
     int kind, first, count, pad;
@@ -161,6 +164,7 @@ struct KParams {
     f4 *sh_c;    // [kMaxLights][n_slots] unoccluded contribution
     f4 *med;     // VPT suspended delta-tracking state: t, t1, ...
     f4 *med2;
+    f4 *nee;     // VPT-NEE suspended ratio tracking, 4 x [n_slots]: (p1, t) (dir, dist) (tr, f) (Le, pdf)
     uint32_t *state, *sample_k, *depth, *occ;
     uint32_t *rng_c, *rng_g, *ring;
     uint32_t *req;             // refill request list (slots)

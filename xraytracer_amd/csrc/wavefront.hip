@@ -543,6 +543,38 @@ __device__ int delta_track(const KParams& P, v3 o, v3 d, v3 thr, float& t, float
     }
 }
 
+// HenyeyGreenstein::evaluate (Src/medium.h:29-34)
+__device__ __forceinline__ float hg_eval(float g, v3 wo, v3 wi) {
+    const float cosTheta = dot(wo, wi);
+    const float denom = 1.0f + g * g - 2.0f * g * cosTheta;
+    return kPI_MUL_4_INV * (1.0f - g * g) / (denom * __builtin_sqrtf(denom));
+}
+
+// HeterogeneousMedium::ratioTrackingTransmittance (Src/medium.h:360-386), resumable like
+// delta_track: false = suspended (fewer than 8 RNG words left); `t`, `tr` carry the loop.
+__device__ bool ratio_track(const KParams& P, v3 p1, v3 dn, float dist, float& t, v3& tr, Rng& rng, uint32_t g) {
+    const DMedium& M = P.medium;
+    const float majorant = M.majorant, invMajorant = M.inv_majorant;
+    const v3 vmaj = mk(majorant, majorant, majorant);
+    const v3 absorb = ld3(M.absorption), scatter = ld3(M.scattering);
+    for (;;) {
+        if (g - rng.c < 8u) return false;
+        const float s = -glibc_logf(smax(1.0f - rng.next(), 0.0f)) * invMajorant;
+        t += s;
+        if (t > dist) return true;
+        const float density = medium_density(M, ray_at(p1, dn, t));
+        const v3 sigma_n = (vmaj - absorb * density) - scatter * density;
+        tr = tr * (sigma_n * invMajorant);
+    }
+}
+
+// VPT-NEE light sample at a scattering point and its resumption (defined with the fused
+// schedule's scene traversal below)
+template <int SCN>
+__device__ int nee_medium(const KParams& P, const LScene& L, uint32_t s, v3 pos, v3 wo, v3 thr_m, v3& rad, Rng& rng,
+                          uint32_t g, uint32_t& nsh);
+__device__ int nee_resume(const KParams& P, uint32_t s, v3 thr_m, v3& rad, Rng& rng, uint32_t g);
+
 // =================================================================== k_shade ====
 template <int SCN, int INTEG>
 __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __restrict__ list,
@@ -599,14 +631,22 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
             }
 
             // ---- 2. shade the traced extension ray (or resume a suspended medium walk)
-            if (INTEG == XRT_INTEGRATOR_VPT && (st & (ST_RAY | ST_MEDIUM))) {
-                // VolumePathTracing::integrate loop body (Src/integrator.h:418-469)
+            if (vpt_family(INTEG) && (st & (ST_RAY | ST_MEDIUM | ST_NEEWALK))) {
+                // VolumePathTracing::integrate loop body (Src/integrator.h:418-469);
+                // VolumePathTracingNEE (:497-581)
                 o = xyz(P.ray_o[s]);
                 d = xyz(P.ray_d[s]);
                 bool walk = false;
                 float mt = 0.0f, mt1 = 0.0f;
                 v3 tt = mk(1, 1, 1), sa = mk(0, 0, 0);
-                if (st & ST_MEDIUM) {
+                if (INTEG == XRT_INTEGRATOR_VPT_NEE && (st & ST_NEEWALK)) {
+                    // suspended NEE ratio tracking; the path ray after the scatter is stored
+                    if (nee_resume(P, s, thr, rad, rng, g) == 0) {
+                        st &= ~ST_NEEWALK;
+                        if (depth < P.max_depth) st |= ST_RAY;
+                        else finalize = true;
+                    }
+                } else if (st & ST_MEDIUM) {
                     st &= ~ST_MEDIUM;
                     const f4 m1 = P.med[s], m2 = P.med2[s];
                     mt = m1.x, mt1 = m1.y, sa = mk(m1.z, m1.w, m2.w), tt = xyz(m2);
@@ -630,7 +670,8 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
                         }
                         const DObj ob = P.objs[obj];
                         if (alive && ob.light >= 0) {
-                            rad = rad + thr * light_Le(P.lights[ob.light], S.ns, d);
+                            if (INTEG == XRT_INTEGRATOR_VPT || depth == 0)
+                                rad = rad + thr * light_Le(P.lights[ob.light], S.ns, d);
                             alive = false, finalize = true;
                         }
                         if (alive) {
@@ -656,11 +697,22 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
                         P.med[s] = make_float4(mt, mt1, sa.x, sa.y);
                         P.med2[s] = make_float4(tt.x, tt.y, tt.z, sa.z);
                     } else {
+                        int nr = 0;
+                        if (INTEG == XRT_INTEGRATOR_VPT_NEE && r == 1) {
+                            LScene Lg;   // the scene in global memory (linear scans, SCN_MIXED)
+                            Lg.tri = P.tri, Lg.tng = P.tri_ng, Lg.nrm = P.tri_nrm, Lg.box = P.obj_box;
+                            Lg.sph = P.sph, Lg.sobj = P.sph_obj, Lg.bx = P.box, Lg.obj = P.objs, Lg.light = P.lights;
+                            nr = nee_medium<SCN>(P, Lg, s, pos, d, thr * tm, rad, rng, g, nsh);
+                        }
                         o = pos;
                         d = dir;
                         thr = thr * tm;
                         if (r == 1) ++depth;
-                        if (depth < P.max_depth) {
+                        if (nr == 2) {
+                            st |= ST_NEEWALK;   // resumes after the refill
+                            P.ray_o[s] = pk(o);
+                            P.ray_d[s] = pk(d);
+                        } else if (depth < P.max_depth) {
                             st |= ST_RAY;
                             P.ray_o[s] = pk(o);
                             P.ray_d[s] = pk(d);
@@ -1083,6 +1135,80 @@ __device__ __forceinline__ int surface_l(const LScene& L, v3 o, v3 d, const HitR
     return __float_as_int(L.bx[2 * idx].w);
 }
 
+// object index of a hit record (see surface_l)
+__device__ __forceinline__ int hit_object(const LScene& L, const HitRec& h) {
+    const int kind = h.code >> 28, idx = h.code & 0x0fffffff;
+    if (kind == SEG_TRI) return __float_as_int(L.tri[3 * idx].w);
+    if (kind == SEG_SPHERE) return L.sobj[idx] & 0x3fffffff;
+    return __float_as_int(L.bx[2 * idx].w);
+}
+
+// VolumePathTracingNEE's light sample at a scattering point (Src/integrator.h:539-560):
+// sampleDirectionToLight (:586-602, Scene::sampleAreaLight Src/scene.cpp:182-188) and
+// isVisible (:604-631) — the shadow ray's closest hit; a surface occludes, a medium
+// attenuates by ratio tracking between the hit's t and t1.  Adds
+// (thr * tm) * (transmittance * f * Le / pdf) to rad and returns 0, or returns 2 with the
+// ratio tracking suspended (state in P.nee, resumed by nee_resume).  Media make a scene
+// SCN_MIXED, so other scene kinds never get here.
+template <int SCN>
+__device__ int nee_medium(const KParams& P, const LScene& L, uint32_t s, v3 pos, v3 wo, v3 thr_m, v3& rad, Rng& rng,
+                          uint32_t g, uint32_t& nsh) {
+    if (SCN != SCN_MIXED) return 0;
+    uint32_t li = (uint32_t)((float)P.n_lights * rng.next());   // size() * getNext1D(), truncated
+    if (li == (uint32_t)P.n_lights) li--;
+    const float choose = 1.0f / (float)P.n_lights;
+    v3 wl = mk(0, 0, 0);
+    float lpdf = 0.0f, dist = 0.0f;
+    const v3 Le = light_sample(L.light[li], pos, wl, lpdf, dist, rng);
+    const float pdf_dir = choose * lpdf;
+    if (!(pdf_dir > 0.0f)) return 0;
+    ++nsh;
+    HitRec h;
+#ifdef XRT_COUNT_TESTS
+    uint32_t cl = 0, cw = 0;
+    closest_l<SCN>(P, L, pos, wl, h, cl, cw);
+#else
+    closest_l<SCN>(P, L, pos, wl, h);
+#endif
+    v3 tr = mk(1, 1, 1);
+    const float f = hg_eval(P.medium.g, wo, wl);
+    if (h.code >= 0) {
+        const DObj ob = L.obj[hit_object(L, h)];
+        if (ob.material != XRT_MAT_NONE) return 0;   // hasSurface(): occluded
+        if (ob.medium >= 0) {
+            const v3 p1 = ray_at(pos, wl, h.t), p2 = ray_at(pos, wl, h.t1);
+            const float dist_end = length(p1 - p2);
+            const v3 dn = normalize(p2 - p1);
+            float t = 0.0f;
+            if (!ratio_track(P, p1, dn, dist_end, t, tr, rng, g)) {
+                const size_t n = P.n_slots;
+                P.nee[s] = make_float4(p1.x, p1.y, p1.z, t);
+                P.nee[n + s] = make_float4(dn.x, dn.y, dn.z, dist_end);
+                P.nee[2 * n + s] = make_float4(tr.x, tr.y, tr.z, f);
+                P.nee[3 * n + s] = make_float4(Le.x, Le.y, Le.z, pdf_dir);
+                return 2;
+            }
+        }
+    }
+    rad = rad + thr_m * (((tr * f) * Le) / pdf_dir);
+    return 0;
+}
+
+// resume a suspended NEE ratio tracking; thr_m = the path throughput after the scatter
+__device__ int nee_resume(const KParams& P, uint32_t s, v3 thr_m, v3& rad, Rng& rng, uint32_t g) {
+    const size_t n = P.n_slots;
+    const f4 a = P.nee[s], b = P.nee[n + s], c = P.nee[2 * n + s], d = P.nee[3 * n + s];
+    float t = a.w;
+    v3 tr = xyz(c);
+    if (!ratio_track(P, xyz(a), xyz(b), b.w, t, tr, rng, g)) {
+        P.nee[s] = make_float4(a.x, a.y, a.z, t);
+        P.nee[2 * n + s] = make_float4(tr.x, tr.y, tr.z, c.w);
+        return 2;
+    }
+    rad = rad + thr_m * (((tr * c.w) * xyz(d)) / d.w);
+    return 0;
+}
+
 #ifndef XRT_STEP_WAVES
 #define XRT_STEP_WAVES 4   // min waves per SIMD the compiler must fit k_step into (<= 128 VGPRs)
 #endif
@@ -1165,13 +1291,21 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
                 thr = mk(1, 1, 1), rad = mk(0, 0, 0);
                 depth = 0;
                 if (!one_hit(INTEG) && P.max_depth == 0) ended = true, trace = false;
-            } else if (INTEG == XRT_INTEGRATOR_VPT && (st & ST_MEDIUM)) {
+            } else if (vpt_family(INTEG) && (st & ST_MEDIUM)) {
                 trace = false;
+            } else if (INTEG == XRT_INTEGRATOR_VPT_NEE && (st & ST_NEEWALK)) {
+                // the previous launch suspended this path's NEE ratio tracking
+                trace = false;
+                if (nee_resume(P, s, thr, rad, rng, g) == 0) {
+                    st &= ~ST_NEEWALK;
+                    if (depth >= P.max_depth) ended = true;
+                    else trace = true;
+                }
             }
             bool walk = false;
             float mt = 0.0f, mt1 = 0.0f;
             v3 tt = mk(1, 1, 1), sa = mk(0, 0, 0);
-            if (INTEG == XRT_INTEGRATOR_VPT && (st & ST_MEDIUM)) {
+            if (vpt_family(INTEG) && (st & ST_MEDIUM)) {
                 st &= ~ST_MEDIUM;
                 const f4 m1 = P.med[s], m2 = P.med2[s];
                 mt = m1.x, mt1 = m1.y, sa = mk(m1.z, m1.w, m2.w), tt = xyz(m2);
@@ -1205,8 +1339,9 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
                         }
                     }
                     ended = true;
-                } else if (INTEG == XRT_INTEGRATOR_VPT) {
-                    // VolumePathTracing::integrate loop body (Src/integrator.h:418-469)
+                } else if (vpt_family(INTEG)) {
+                    // VolumePathTracing::integrate loop body (Src/integrator.h:418-469);
+                    // VolumePathTracingNEE (:497-581): Le only at depth 0
                     if (obj < 0) {
                         rad = rad + (thr * mk(0.0f, 0.0f, 0.0f)) * (float)(depth != 0);
                         ended = true;
@@ -1219,7 +1354,8 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
                         }
                         const DObj& ob = L.obj[obj];
                         if (alive && ob.light >= 0) {
-                            rad = rad + thr * light_Le(L.light[ob.light], S.ns, d);
+                            if (INTEG == XRT_INTEGRATOR_VPT || depth == 0)
+                                rad = rad + thr * light_Le(L.light[ob.light], S.ns, d);
                             alive = false, ended = true;
                         }
                         if (alive) {
@@ -1291,7 +1427,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
                     }
                 }
             }
-            if (INTEG == XRT_INTEGRATOR_VPT && walk) {
+            if (vpt_family(INTEG) && walk) {
                 v3 pos, dir, tm;
                 const int r = delta_track(P, o, d, thr, mt, mt1, tt, sa, rng, g, pos, dir, tm);
                 if (r == 2) {
@@ -1299,10 +1435,16 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
                     P.med[s] = make_float4(mt, mt1, sa.x, sa.y);
                     P.med2[s] = make_float4(tt.x, tt.y, tt.z, sa.z);
                 } else {
+                    // VolumePathTracingNEE: light sample at a scattering event, before the
+                    // ray advances (Src/integrator.h:537-572)
+                    const int nr = (INTEG == XRT_INTEGRATOR_VPT_NEE && r == 1)
+                                       ? nee_medium<SCN>(P, L, s, pos, d, thr * tm, rad, rng, g, nsh)
+                                       : 0;
                     o = pos, d = dir;
                     thr = thr * tm;
                     if (r == 1) ++depth;
-                    if (depth >= P.max_depth) ended = true;
+                    if (nr == 2) st |= ST_NEEWALK;   // resumes at the next launch (RNG words ran out)
+                    else if (depth >= P.max_depth) ended = true;
                 }
             }
             // finish the sample (Src/renderer.cpp:55-75) and start the next one right away:
@@ -1941,6 +2083,9 @@ static hipError_t shade_i(const KParams& P, const uint32_t* list, const uint32_t
     else if (P.integrator == XRT_INTEGRATOR_NORMAL)
         hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_NORMAL>), dim3(blocks), dim3(kBlock), 0, st, P, list, count,
                            out, out_count, req_count);
+    else if (P.integrator == XRT_INTEGRATOR_VPT_NEE)
+        hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_VPT_NEE>), dim3(blocks), dim3(kBlock), 0, st, P, list, count,
+                           out, out_count, req_count);
     else
         hipLaunchKernelGGL((k_shade<SCN, XRT_INTEGRATOR_GI>), dim3(blocks), dim3(kBlock), 0, st, P, list, count,
                            out, out_count, req_count);
@@ -1979,6 +2124,9 @@ static hipError_t step_i(const KParams& P, const uint32_t* list, const uint32_t*
                            out, out_count, zero, req_count, visits);
     else if (P.integrator == XRT_INTEGRATOR_NORMAL)
         hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_NORMAL>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
+                           out, out_count, zero, req_count, visits);
+    else if (P.integrator == XRT_INTEGRATOR_VPT_NEE)
+        hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_VPT_NEE>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
                            out, out_count, zero, req_count, visits);
     else
         hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_GI>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,

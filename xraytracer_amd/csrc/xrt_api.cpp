@@ -45,7 +45,7 @@ struct xrt_ctx {
     bool has_scene = false, has_camera = false, has_medium = false;
     // slots
     size_t cap_slots = 0;
-    DevBuf ray_o, ray_d, thr, rad, thr_prev, hit, hit2, hit3, sh_o, sh_d, sh_c, med, med2;
+    DevBuf ray_o, ray_d, thr, rad, thr_prev, hit, hit2, hit3, sh_o, sh_d, sh_c, med, med2, nee;
     DevBuf state, sample_k, depth, occ, rng_c, rng_g, ring, c_seg, c_shadow, c_rej, c_stall, lists;
     DevBuf counts, stats, fb, scratch, kparams;
     size_t cap_fb = 0;
@@ -139,7 +139,7 @@ void xrt_destroy(xrt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->tri, &c->tri_ng, &c->tri_nrm, &c->sph, &c->sph_obj, &c->box, &c->objs, &c->lights,
                      &c->segs, &c->density, &c->obj_box, &c->bvh_node, &c->bvh_tri, &c->snode, &c->ssph, &c->sbk, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
-                     &c->hit2, &c->hit3, &c->sh_o, &c->sh_d, &c->sh_c, &c->med, &c->med2, &c->state,
+                     &c->hit2, &c->hit3, &c->sh_o, &c->sh_d, &c->sh_c, &c->med, &c->med2, &c->nee, &c->state,
                      &c->sample_k, &c->depth, &c->occ, &c->rng_c, &c->rng_g, &c->ring, &c->c_seg, &c->c_shadow,
                      &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch, &c->kparams};
     for (DevBuf* b : all) free_buf(*b);
@@ -408,10 +408,13 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     if (!c->has_scene || !c->has_camera) return set_err(c, XRT_ERR_STATE, "upload a scene and set a camera first");
     if (p->width == 0 || p->height == 0 || p->shard_count == 0 || p->shard_index >= p->shard_count)
         return set_err(c, XRT_ERR_INVALID, "bad image size or shard");
-    if (p->integrator < XRT_INTEGRATOR_GI || p->integrator > XRT_INTEGRATOR_NORMAL)
+    if (p->integrator < XRT_INTEGRATOR_GI || p->integrator > XRT_INTEGRATOR_VPT_NEE)
         return set_err(c, XRT_ERR_INVALID, "unknown integrator");
-    if (p->integrator == XRT_INTEGRATOR_VPT && !c->has_medium)
+    const bool volumetric = p->integrator == XRT_INTEGRATOR_VPT || p->integrator == XRT_INTEGRATOR_VPT_NEE;
+    if (volumetric && !c->has_medium)
         return set_err(c, XRT_ERR_STATE, "VolumePathTracing needs xrt_set_medium first");
+    if (p->integrator == XRT_INTEGRATOR_VPT_NEE && c->base.n_lights == 0)
+        return set_err(c, XRT_ERR_STATE, "VolumePathTracingNEE needs an area light");
     HIPCHK(c, hipSetDevice(c->device));
     const uint32_t rows = shard_rows(p->height, p->shard_index, p->shard_count);
     const size_t n = (size_t)rows * p->width;
@@ -424,6 +427,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             (rc = ensure(c, c->hit2, n * 16)) || (rc = ensure(c, c->hit3, n * 16)) ||
             (rc = ensure(c, c->sh_o, L * n * 16)) || (rc = ensure(c, c->sh_d, L * n * 16)) ||
             (rc = ensure(c, c->sh_c, L * n * 16)) || (rc = ensure(c, c->med, n * 16)) || (rc = ensure(c, c->med2, n * 16)) ||
+            (rc = ensure(c, c->nee, 4 * n * 16)) ||
             (rc = ensure(c, c->state, n * 4)) || (rc = ensure(c, c->sample_k, n * 4)) || (rc = ensure(c, c->depth, n * 4)) ||
             (rc = ensure(c, c->occ, n * 4)) || (rc = ensure(c, c->rng_c, n * 4)) || (rc = ensure(c, c->rng_g, n * 4)) ||
             (rc = ensure(c, c->ring, n * kRing * 4)) || (rc = ensure(c, c->c_seg, n * 4)) ||
@@ -453,7 +457,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     P.ray_o = as<f4>(c->ray_o), P.ray_d = as<f4>(c->ray_d), P.thr = as<f4>(c->thr), P.rad = as<f4>(c->rad);
     P.thr_prev = as<f4>(c->thr_prev), P.hit = as<f4>(c->hit), P.hit2 = as<f4>(c->hit2), P.hit3 = as<f4>(c->hit3);
     P.sh_o = as<f4>(c->sh_o), P.sh_d = as<f4>(c->sh_d), P.sh_c = as<f4>(c->sh_c);
-    P.med = as<f4>(c->med), P.med2 = as<f4>(c->med2);
+    P.med = as<f4>(c->med), P.med2 = as<f4>(c->med2), P.nee = as<f4>(c->nee);
     P.state = as<uint32_t>(c->state), P.sample_k = as<uint32_t>(c->sample_k), P.depth = as<uint32_t>(c->depth);
     P.occ = as<uint32_t>(c->occ), P.rng_c = as<uint32_t>(c->rng_c), P.rng_g = as<uint32_t>(c->rng_g);
     P.ring = as<uint32_t>(c->ring);
@@ -517,8 +521,8 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     const uint32_t blocks = P.n_part * ((P.part_cap + 255) / 256);   // one entry per thread
     // GI/Direct: at most max_depth + 1 shade passes per sample; VPT walks are unbounded
     // (null collisions, suspensions), so only the live-slot poll ends the loop there.
-    const uint64_t cap_iters = p->integrator == XRT_INTEGRATOR_VPT ? (uint64_t)p->spp * 100000ull + 1000000ull
-                                                                    : (uint64_t)p->spp * (p->max_depth + 2) + 16;
+    const uint64_t cap_iters = volumetric ? (uint64_t)p->spp * 100000ull + 1000000ull
+                                          : (uint64_t)p->spp * (p->max_depth + 2) + 16;
     // asynchronous termination polling: every kPoll iterations copy the live-slot count to
     // pinned memory; block on a poll only when the host runs kAhead iterations ahead.
     constexpr uint64_t kPoll = 16, kAhead = 64;
