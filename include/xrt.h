@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 5
+#define XRT_ABI_VERSION 6
 
 /* ---- status codes ---------------------------------------------------------------- */
 enum {
@@ -84,9 +84,19 @@ typedef struct {
     const xrt_light* lights;
 } xrt_scene_desc;
 
-/* Dense density grid standing in for DensityGrid (Src/grid.h:9-15): OpenVDB
+/* The scene medium.  kind XRT_MEDIUM_HETEROGENEOUS: HeterogeneousMedium over a dense
+ * density grid standing in for DensityGrid (Src/grid.h:9-15): OpenVDB
  * BoxSampler::wsSample semantics — world -> index by (p - origin) / voxel_size, voxel
- * centres at integer index coordinates, trilinear, background 0 outside the data. */
+ * centres at integer index coordinates, trilinear, background 0 outside the data.
+ * The homogeneous kinds (Src/medium.h:122-277) use absorption / scattering as sigma_a /
+ * sigma_s (Achromatic: channel 0 of each), bbox as the medium box and g; the grid fields
+ * (nx..voxel_size, max_density, density_multiplier) are ignored and density may be NULL. */
+enum {
+    XRT_MEDIUM_HETEROGENEOUS = 0,          /* HeterogeneousMedium (delta / ratio tracking)  */
+    XRT_MEDIUM_HOMOGENEOUS_MIS = 1,        /* HomogeneousMediumMIS (Src/medium.h:148-192)   */
+    XRT_MEDIUM_HOMOGENEOUS_ACHROMATIC = 2, /* HomogeneousMediumAchromatic (:195-231)        */
+    XRT_MEDIUM_HOMOGENEOUS_NOMIS = 3       /* HomogeneousMediumNoMIS (:234-277)             */
+};
 typedef struct {
     uint32_t nx, ny, nz;
     const float* density;    /* [nz][ny][nx]                                           */
@@ -99,6 +109,7 @@ typedef struct {
     float absorption[3];     /* HeterogeneousMedium::absorptionColor                    */
     float scattering[3];     /* HeterogeneousMedium::scatteringColor                    */
     float density_multiplier;
+    int32_t kind;            /* XRT_MEDIUM_* (0 when zero-initialised: heterogeneous)   */
 } xrt_medium_desc;
 
 /* ---- render parameters --------------------------------------------------------------- */

@@ -29,7 +29,9 @@ public:
     // ---- additions for the GPU backend ----
     // Flattened, in m_objects iteration order; valid until the scene changes.
     int flatten(xrt_scene_desc* out) const;
-    // the one medium referenced by objects (VolumePathTracing scenes), or nullptr
+    // the one medium referenced by objects (VolumePathTracing scenes), or nullptr;
+    // medium() only when it is a HeterogeneousMedium
+    const Medium* anyMedium() const;
     const HeterogeneousMedium* medium() const;
     std::vector<std::string> objectNames() const;
     const std::string& lastError() const { return m_error; }

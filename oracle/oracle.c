@@ -527,6 +527,78 @@ static int sample_medium(const scene_ctx* C, v3 ro, v3 rd, v3 rthr, const hinfo*
     }
 }
 
+/* Homogeneous media (Src/medium.h:122-277): one free-flight sample, analytic
+ * transmittance exp(-sigma_t * t).  Returns 1 on a scattering event. */
+static inline v3 analytic_tr(float t, v3 sigma_t) {   /* Medium::analyticTransmittance */
+    return vexp(vmuls(vneg(sigma_t), t));
+}
+static int homog_sample_medium(const xrt_medium_desc* M, v3 ro, v3 rd, v3 rthr, const hinfo* info, orc_mt* rng,
+                               v3* pos, v3* dir, v3* throughput, uint64_t* ub) {
+    const v3 sa = ld3(M->absorption), ss = ld3(M->scattering), st = vadd(sa, ss);
+    const float distToSurface = info->t1 - info->t;
+    if (M->kind == XRT_MEDIUM_HOMOGENEOUS_MIS) {
+        /* HomogeneousMediumMIS::sampleMedium (Src/medium.h:154-191) */
+        v3 pmf;
+        const uint32_t channel = sample_wavelength(rthr, vdivv(ss, st), rng, &pmf, ub);
+        const float t = -logf(smax(1.0f - orc_draw(rng), 0.0f)) / comp(st, (int)channel);
+        if (t > distToSurface - RAY_EPS) {
+            *pos = ray_at(ro, rd, info->t1 + RAY_EPS);
+            *dir = rd;
+            const v3 tr = analytic_tr(distToSurface, st);
+            const v3 pdf = vmul(pmf, tr);
+            *throughput = vdivs(tr, pdf.x + pdf.y + pdf.z);
+            return 0;
+        }
+        hg_sample(M->g, rd, rng, dir);
+        *pos = ray_at(ro, rd, info->t + t);
+        const v3 tr = analytic_tr(t, st);
+        const v3 pdf = vmul(pmf, vmul(st, tr));
+        *throughput = vdivs(vmul(tr, ss), pdf.x + pdf.y + pdf.z);
+        return 1;
+    }
+    if (M->kind == XRT_MEDIUM_HOMOGENEOUS_ACHROMATIC) {
+        /* HomogeneousMediumAchromatic::sampleMedium (Src/medium.h:201-229) */
+        const float t = -logf(smax(1.0f - orc_draw(rng), 0.0f)) / st.x;
+        if (t > distToSurface - RAY_EPS) {
+            *pos = ray_at(ro, rd, info->t1 + RAY_EPS);
+            *dir = rd;
+            *throughput = mk(1.0f, 1.0f, 1.0f);
+            return 0;
+        }
+        hg_sample(M->g, rd, rng, dir);
+        *pos = ray_at(ro, rd, info->t + t);
+        *throughput = vdivv(ss, st);
+        return 1;
+    }
+    /* HomogeneousMediumNoMIS::sampleMedium (Src/medium.h:240-275) */
+    int channel = (int)(3 * orc_draw(rng));
+    if (channel == 3) channel--;
+    const float pmf_wavelength = 1.0f / 3.0f;
+    const float sc = comp(st, channel);
+    const float t = -logf(smax(1.0f - orc_draw(rng), 0.0f)) / sc;
+    const float pdf_distance = sc * expf(-sc * t);
+    if (t > distToSurface - RAY_EPS) {
+        *pos = ray_at(ro, rd, info->t1 + RAY_EPS);
+        *dir = rd;
+        const v3 tr = analytic_tr(distToSurface, st);
+        const float p_surface = expf(-sc * distToSurface);
+        *throughput = vdivs(vmuls(tr, 1.0f / 3.0f), pmf_wavelength * p_surface);
+        return 0;
+    }
+    hg_sample(M->g, rd, rng, dir);
+    *pos = ray_at(ro, rd, info->t + t);
+    *throughput = vdivs(vmul(vmuls(analytic_tr(t, st), 1.0f / 3.0f), ss), pmf_wavelength * pdf_distance);
+    return 1;
+}
+
+/* Object::sampleMedium -> the scene medium's sampleMedium */
+static int medium_sample(const scene_ctx* C, v3 ro, v3 rd, v3 rthr, const hinfo* info, orc_mt* rng, v3* pos,
+                         v3* dir, v3* throughput, uint64_t* ub) {
+    if (C->M->kind != XRT_MEDIUM_HETEROGENEOUS)
+        return homog_sample_medium(C->M, ro, rd, rthr, info, rng, pos, dir, throughput, ub);
+    return sample_medium(C, ro, rd, rthr, info, rng, pos, dir, throughput, ub);
+}
+
 /* ---------------------------------------------------------------- integrators ---- */
 typedef struct {
     uint64_t segments, shadow_rays, tri_tests, stalled, ub_channel;
@@ -704,7 +776,7 @@ static v3 integrate_vpt(const scene_ctx* C, v3 ro, v3 rd, uint32_t max_depth, or
         }
         if (ob->medium >= 0 && C->M) {
             v3 pos, dir, tm;
-            int scattered = sample_medium(C, ro, rd, thr, &info, rng, &pos, &dir, &tm, &pc->ub_channel);
+            int scattered = medium_sample(C, ro, rd, thr, &info, rng, &pos, &dir, &tm, &pc->ub_channel);
             ro = pos;
             rd = dir;
             thr = vmul(thr, tm);
@@ -768,7 +840,7 @@ static v3 integrate_vpt_nee(const scene_ctx* C, v3 ro, v3 rd, uint32_t max_depth
         }
         if (ob->medium >= 0 && C->M) {
             v3 pos, dir, tm;
-            const int scattered = sample_medium(C, ro, rd, thr, &info, rng, &pos, &dir, &tm, &pc->ub_channel);
+            const int scattered = medium_sample(C, ro, rd, thr, &info, rng, &pos, &dir, &tm, &pc->ub_channel);
             if (scattered) {
                 /* light index: (unsigned)(size * u), clamped; pdf 1 / size */
                 unsigned li = (unsigned)((float)S->n_lights * orc_draw(rng));
@@ -789,7 +861,14 @@ static v3 integrate_vpt_nee(const scene_ctx* C, v3 ro, v3 rd, uint32_t max_depth
                         if (so->material != XRT_MAT_NONE) {
                             visible = 0;
                         } else if (so->medium >= 0) {
-                            transmittance = vmul(transmittance, ratio_tracking(C, ray_at(pos, wl, sh.t), ray_at(pos, wl, sh.t1), rng));
+                            const v3 p1 = ray_at(pos, wl, sh.t), p2 = ray_at(pos, wl, sh.t1);
+                            /* Medium::transmittance: ratio tracking (heterogeneous) or
+                             * analyticTransmittance(length(p1 - p2), sigma_t) (Src/medium.h:133-137) */
+                            transmittance = vmul(transmittance,
+                                                 C->M->kind == XRT_MEDIUM_HETEROGENEOUS
+                                                     ? ratio_tracking(C, p1, p2, rng)
+                                                     : analytic_tr(vlength(vsub(p1, p2)),
+                                                                   vadd(ld3(C->M->absorption), ld3(C->M->scattering))));
                         }
                     }
                     if (visible) {
@@ -817,7 +896,7 @@ static int setup_ctx(scene_ctx* C, const xrt_scene_desc* S, const xrt_medium_des
     C->M = M;
     C->majorant = 0.0f;
     C->inv_majorant = 0.0f;
-    if (M) {
+    if (M && M->kind == XRT_MEDIUM_HETEROGENEOUS) {
         /* HeterogeneousMedium ctor (Src/medium.cpp:5-17) */
         const float max_density = M->density_multiplier * M->max_density;
         const v3 m = vadd(vmuls(ld3(M->absorption), max_density), vmuls(ld3(M->scattering), max_density));

@@ -373,6 +373,32 @@ def dense_smoke(w, h, n=24, g=0.4):
     return s
 
 
+def homog_scene(kind, w, h, g=0.3):
+    """A homogeneous medium box (HomogeneousMedium{MIS,Achromatic,NoMIS}, Src/medium.h:
+    122-277) under a quad light."""
+    s = scenes.SceneBundle()
+    a = (0.02, 0.02, 0.02) if kind == "achromatic" else (0.02, 0.03, 0.01)
+    sc = (0.08, 0.08, 0.08) if kind == "achromatic" else (0.06, 0.09, 0.12)
+    s.add_quad_light("QuadLight", (18.0, 25.0, 18.0), (2.0, 25.0, 18.0), (18.0, 25.0, 2.0), (20.0, 20.0, 20.0))
+    s.add_medium("medium", scenes.HomogeneousMedium(kind, g, a, sc, (0.0, 0.0, 0.0), (20.0, 12.0, 20.0)))
+    s.flatten()
+    s.camera = scenes.pinhole((1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 10, 6, 55, 1), 45.0, w, h)
+    s.integrator, s.max_depth = "vpt", 10
+    return s
+
+
+@pytest.mark.parametrize("kind", ["mis", "achromatic", "nomis"])
+@pytest.mark.parametrize("integ", ["vpt", "vpt_nee"])
+def test_homogeneous_media(renderer, sched, kind, integ):
+    """Homogeneous media under VolumePathTracing and VolumePathTracingNEE (analytic
+    transmittance on the NEE shadow ray), bit-exact against the oracle."""
+    s = homog_scene(kind, 40, 30)
+    img, ref, st = render_both(renderer, s, 40, 30, 4, integrator=integ, schedule=sched)
+    compare(img, ref)
+    g = renderer.stats
+    assert g.draws == st["draws"] and g.segments == st["segments"] and g.shadow_rays == st["shadow_rays"]
+
+
 @pytest.mark.parametrize("dense", [False, True])
 def test_vpt_nee(renderer, sched, dense):
     """VolumePathTracingNEE (Src/integrator.h:481-636): light sample at every scattering

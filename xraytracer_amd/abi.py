@@ -16,13 +16,14 @@ LIB_PATH = os.path.join(HERE, "libxrt_hip.so")
 if os.environ.get("XRT_LIB"):   # experiment builds (csrc/Makefile `variant`), same ABI
     LIB_PATH = os.path.join(HERE, os.environ["XRT_LIB"])
 
-XRT_ABI_VERSION = 5   # include/xrt.h XRT_ABI_VERSION
+XRT_ABI_VERSION = 6   # include/xrt.h XRT_ABI_VERSION
 XRT_OK = 0
 XRT_OBJ_MESH, XRT_OBJ_SPHERE, XRT_OBJ_BOX = 0, 1, 2
 XRT_LIGHT_QUAD, XRT_LIGHT_TRIANGLE, XRT_LIGHT_SPHERE = 0, 1, 2
 XRT_MAT_NONE, XRT_MAT_LAMBERT = 0, 1
 XRT_INTEGRATOR_GI, XRT_INTEGRATOR_DIRECT, XRT_INTEGRATOR_VPT = 0, 1, 2
 XRT_INTEGRATOR_INDIRECT, XRT_INTEGRATOR_NORMAL, XRT_INTEGRATOR_VPT_NEE = 3, 4, 5
+XRT_MEDIUM_HETEROGENEOUS, XRT_MEDIUM_HOMOGENEOUS_MIS, XRT_MEDIUM_HOMOGENEOUS_ACHROMATIC, XRT_MEDIUM_HOMOGENEOUS_NOMIS = 0, 1, 2, 3
 XRT_FLAG_TIMING, XRT_FLAG_WAVEFRONT, XRT_FLAG_NO_MERGED = 1, 2, 4
 XRT_SCHED_WAVEFRONT, XRT_SCHED_STEP, XRT_SCHED_STEP_TRI, XRT_SCHED_STEP_MERGED = 0, 1, 2, 3
 SCHEDULE_NAMES = ("wavefront", "step", "step_tri", "step_merged")
@@ -62,7 +63,7 @@ class XrtMediumDesc(C.Structure):
                 ("bbox_min", C.c_float * 3), ("bbox_max", C.c_float * 3),
                 ("max_density", C.c_float), ("g", C.c_float),
                 ("absorption", C.c_float * 3), ("scattering", C.c_float * 3),
-                ("density_multiplier", C.c_float)]
+                ("density_multiplier", C.c_float), ("kind", C.c_int32)]
 
 
 class XrtRenderParams(C.Structure):

@@ -48,7 +48,22 @@ void HipRenderer::render(const Scene& scene, Sampler::SamplerType, Image& image)
         case Integrator::Kind::Normal: p.integrator = XRT_INTEGRATOR_NORMAL; break;
         case Integrator::Kind::VolumePathTracingNEE: p.integrator = XRT_INTEGRATOR_VPT_NEE; break;
     }
-    if (p.integrator == XRT_INTEGRATOR_VPT || p.integrator == XRT_INTEGRATOR_VPT_NEE) {
+    const HomogeneousMedium* hom = dynamic_cast<const HomogeneousMedium*>(scene.anyMedium());
+    if ((p.integrator == XRT_INTEGRATOR_VPT || p.integrator == XRT_INTEGRATOR_VPT_NEE) && hom) {
+        xrt_medium_desc md;
+        std::memset(&md, 0, sizeof(md));
+        md.kind = dynamic_cast<const HomogeneousMediumAchromatic*>(hom) ? XRT_MEDIUM_HOMOGENEOUS_ACHROMATIC
+                  : dynamic_cast<const HomogeneousMediumNoMIS*>(hom)    ? XRT_MEDIUM_HOMOGENEOUS_NOMIS
+                                                                        : XRT_MEDIUM_HOMOGENEOUS_MIS;
+        for (int c = 0; c < 3; ++c) {
+            md.bbox_min[c] = hom->bounds().pMin[c];
+            md.bbox_max[c] = hom->bounds().pMax[c];
+            md.absorption[c] = hom->sigmaA()[c];
+            md.scattering[c] = hom->sigmaS()[c];
+        }
+        md.g = hom->g();
+        if ((rc = xrt_set_medium(m_ctx, &md)) != XRT_OK) return fail(rc, "xrt_set_medium");
+    } else if (p.integrator == XRT_INTEGRATOR_VPT || p.integrator == XRT_INTEGRATOR_VPT_NEE) {
         const HeterogeneousMedium* med = scene.medium();
         const DenseGrid* grid = med ? dynamic_cast<const DenseGrid*>(med->grid()) : nullptr;
         if (!grid) return fail(XRT_ERR_UNSUPPORTED, "VolumePathTracing needs a HeterogeneousMedium over a DenseGrid");

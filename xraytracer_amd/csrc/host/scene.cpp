@@ -482,11 +482,13 @@ std::vector<std::string> Scene::objectNames() const {
     return n;
 }
 
-const HeterogeneousMedium* Scene::medium() const {
+const Medium* Scene::anyMedium() const {
     for (const auto& kv : m_objects)
-        if (kv.second->medium()) return dynamic_cast<const HeterogeneousMedium*>(kv.second->medium());
+        if (kv.second->medium()) return kv.second->medium();
     return nullptr;
 }
+
+const HeterogeneousMedium* Scene::medium() const { return dynamic_cast<const HeterogeneousMedium*>(anyMedium()); }
 
 static void put3(float* d, const Vec3f& v) {
     d[0] = v[0];

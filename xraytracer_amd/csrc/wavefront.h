@@ -118,6 +118,8 @@ struct DMedium {
     float origin[3], voxel_size;
     float absorption[3], scattering[3], multiplier, g;
     float majorant, inv_majorant;
+    int kind;              // XRT_MEDIUM_* (0 heterogeneous: delta / ratio tracking)
+    float sigma_t[3];      // homogeneous kinds: sigma_a + sigma_s (HomogeneousMedium ctor)
 };
 
 #ifdef __HIPCC__

@@ -575,6 +575,71 @@ __device__ int nee_medium(const KParams& P, const LScene& L, uint32_t s, v3 pos,
                           uint32_t g, uint32_t& nsh);
 __device__ int nee_resume(const KParams& P, uint32_t s, v3 thr_m, v3& rad, Rng& rng, uint32_t g);
 
+// Homogeneous media (Src/medium.h:122-277): one free-flight sample per visit of the medium
+// box, analytic transmittance exp(-sigma_t * t) (Medium::analyticTransmittance).  Same
+// return contract as delta_track (0 = left the medium, 1 = scattering); never suspends
+// (at most 4 draws).  t, t1: the box hit's entry / exit (IntersectInfo t, t1).
+__device__ __forceinline__ v3 analytic_tr(float t, v3 sigma_t) { return vexp((-sigma_t) * t); }
+__device__ int homog_track(const KParams& P, v3 o, v3 d, v3 thr, float t0, float t1, Rng& rng, v3& pos, v3& dir,
+                           v3& tm) {
+    const DMedium& M = P.medium;
+    const v3 ss = ld3(M.scattering), st = ld3(M.sigma_t);
+    const float distToSurface = t1 - t0;
+    if (M.kind == XRT_MEDIUM_HOMOGENEOUS_MIS) {
+        // HomogeneousMediumMIS::sampleMedium (Src/medium.h:154-191)
+        v3 pmf;
+        const uint32_t channel = sample_wavelength(thr, ss / st, rng, pmf);
+        const float t = -glibc_logf(smax(1.0f - rng.next(), 0.0f)) / comp(st, channel);
+        if (t > distToSurface - kRAY_EPS) {
+            pos = ray_at(o, d, t1 + kRAY_EPS);
+            dir = d;
+            const v3 tr = analytic_tr(distToSurface, st);
+            const v3 pdf = pmf * tr;
+            tm = tr / (pdf.x + pdf.y + pdf.z);
+            return 0;
+        }
+        hg_sample(M.g, d, rng, dir);
+        pos = ray_at(o, d, t0 + t);
+        const v3 tr = analytic_tr(t, st);
+        const v3 pdf = pmf * (st * tr);
+        tm = (tr * ss) / (pdf.x + pdf.y + pdf.z);
+        return 1;
+    }
+    if (M.kind == XRT_MEDIUM_HOMOGENEOUS_ACHROMATIC) {
+        // HomogeneousMediumAchromatic::sampleMedium (Src/medium.h:201-229)
+        const float t = -glibc_logf(smax(1.0f - rng.next(), 0.0f)) / st.x;
+        if (t > distToSurface - kRAY_EPS) {
+            pos = ray_at(o, d, t1 + kRAY_EPS);
+            dir = d;
+            tm = mk(1.0f, 1.0f, 1.0f);
+            return 0;
+        }
+        hg_sample(M.g, d, rng, dir);
+        pos = ray_at(o, d, t0 + t);
+        tm = ss / st;
+        return 1;
+    }
+    // HomogeneousMediumNoMIS::sampleMedium (Src/medium.h:240-275)
+    int channel = (int)(3.0f * rng.next());
+    if (channel == 3) channel--;
+    const float pmf_wavelength = 1.0f / 3.0f;
+    const float sc = comp(st, (uint32_t)channel);
+    const float t = -glibc_logf(smax(1.0f - rng.next(), 0.0f)) / sc;
+    const float pdf_distance = sc * glibc_expf(-sc * t);
+    if (t > distToSurface - kRAY_EPS) {
+        pos = ray_at(o, d, t1 + kRAY_EPS);
+        dir = d;
+        const v3 tr = analytic_tr(distToSurface, st);
+        const float p_surface = glibc_expf(-sc * distToSurface);
+        tm = (tr * (1.0f / 3.0f)) / (pmf_wavelength * p_surface);
+        return 0;
+    }
+    hg_sample(M.g, d, rng, dir);
+    pos = ray_at(o, d, t0 + t);
+    tm = ((analytic_tr(t, st) * (1.0f / 3.0f)) * ss) / (pmf_wavelength * pdf_distance);
+    return 1;
+}
+
 // =================================================================== k_shade ====
 template <int SCN, int INTEG>
 __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __restrict__ list,
@@ -678,7 +743,8 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
                             if (ob.medium >= 0) {
                                 // sampleMedium entry (Src/medium.cpp:47-52): t = info.t
                                 mt = h.x, mt1 = t1;
-                                sa = ld3(P.medium.absorption) * medium_density(P.medium, ray_at(o, d, mt));
+                                if (P.medium.kind == XRT_MEDIUM_HETEROGENEOUS)
+                                    sa = ld3(P.medium.absorption) * medium_density(P.medium, ray_at(o, d, mt));
                                 walk = true;
                             } else {
                                 // neither light nor medium: the reference never advances this
@@ -691,7 +757,9 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
                 }
                 if (walk) {
                     v3 pos, dir, tm;
-                    const int r = delta_track(P, o, d, thr, mt, mt1, tt, sa, rng, g, pos, dir, tm);
+                    const int r = P.medium.kind == XRT_MEDIUM_HETEROGENEOUS
+                                      ? delta_track(P, o, d, thr, mt, mt1, tt, sa, rng, g, pos, dir, tm)
+                                      : homog_track(P, o, d, thr, mt, mt1, rng, pos, dir, tm);
                     if (r == 2) {
                         st |= ST_MEDIUM;
                         P.med[s] = make_float4(mt, mt1, sa.x, sa.y);
@@ -1175,7 +1243,11 @@ __device__ int nee_medium(const KParams& P, const LScene& L, uint32_t s, v3 pos,
     if (h.code >= 0) {
         const DObj ob = L.obj[hit_object(L, h)];
         if (ob.material != XRT_MAT_NONE) return 0;   // hasSurface(): occluded
-        if (ob.medium >= 0) {
+        if (ob.medium >= 0 && P.medium.kind != XRT_MEDIUM_HETEROGENEOUS) {
+            // HomogeneousMedium::transmittance (Src/medium.h:133-137)
+            const v3 p1 = ray_at(pos, wl, h.t), p2 = ray_at(pos, wl, h.t1);
+            tr = tr * analytic_tr(length(p1 - p2), ld3(P.medium.sigma_t));
+        } else if (ob.medium >= 0) {
             const v3 p1 = ray_at(pos, wl, h.t), p2 = ray_at(pos, wl, h.t1);
             const float dist_end = length(p1 - p2);
             const v3 dn = normalize(p2 - p1);
@@ -1361,7 +1433,8 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
                         if (alive) {
                             if (ob.medium >= 0) {
                                 mt = h.t, mt1 = h.t1;
-                                sa = ld3(P.medium.absorption) * medium_density(P.medium, ray_at(o, d, mt));
+                                if (P.medium.kind == XRT_MEDIUM_HETEROGENEOUS)
+                                    sa = ld3(P.medium.absorption) * medium_density(P.medium, ray_at(o, d, mt));
                                 walk = true;
                             } else {
                                 ++nstall;   // see k_shade: the reference never advances this ray
@@ -1429,7 +1502,9 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
             }
             if (vpt_family(INTEG) && walk) {
                 v3 pos, dir, tm;
-                const int r = delta_track(P, o, d, thr, mt, mt1, tt, sa, rng, g, pos, dir, tm);
+                const int r = P.medium.kind == XRT_MEDIUM_HETEROGENEOUS
+                                  ? delta_track(P, o, d, thr, mt, mt1, tt, sa, rng, g, pos, dir, tm)
+                                  : homog_track(P, o, d, thr, mt, mt1, rng, pos, dir, tm);
                 if (r == 2) {
                     st |= ST_MEDIUM;
                     P.med[s] = make_float4(mt, mt1, sa.x, sa.y);

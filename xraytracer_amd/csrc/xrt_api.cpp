@@ -375,7 +375,22 @@ int xrt_set_camera(xrt_ctx* c, const float c2w[16], float scale, float aspect) {
 }
 
 int xrt_set_medium(xrt_ctx* c, const xrt_medium_desc* m) {
-    if (!c || !m || !m->density || !m->nx || !m->ny || !m->nz) return XRT_ERR_INVALID;
+    if (!c || !m) return XRT_ERR_INVALID;
+    if (m->kind != XRT_MEDIUM_HETEROGENEOUS) {
+        // HomogeneousMedium{MIS, Achromatic, NoMIS} (Src/medium.h:122-277): sigma_t = a + s
+        if (m->kind > XRT_MEDIUM_HOMOGENEOUS_NOMIS || m->kind < 0) return set_err(c, XRT_ERR_INVALID, "bad medium kind");
+        DMedium& D = c->base.medium;
+        D = DMedium{};
+        D.kind = m->kind;
+        D.g = m->g;
+        const Vec3f a(m->absorption[0], m->absorption[1], m->absorption[2]);
+        const Vec3f sc(m->scattering[0], m->scattering[1], m->scattering[2]);
+        const Vec3f t = a + sc;
+        for (int q = 0; q < 3; ++q) D.absorption[q] = a[q], D.scattering[q] = sc[q], D.sigma_t[q] = t[q];
+        c->has_medium = true;
+        return XRT_OK;
+    }
+    if (!m->density || !m->nx || !m->ny || !m->nz) return XRT_ERR_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     const size_t n = (size_t)m->nx * m->ny * m->nz;
     int rc = upload(c, c->density, m->density, n * sizeof(float));
@@ -391,6 +406,7 @@ int xrt_set_medium(xrt_ctx* c, const xrt_medium_desc* m) {
     D.voxel_size = m->voxel_size;
     D.multiplier = m->density_multiplier;
     D.g = m->g;
+    D.kind = XRT_MEDIUM_HETEROGENEOUS;
     // HeterogeneousMedium ctor (Src/medium.cpp:5-17)
     const float max_density = m->density_multiplier * m->max_density;
     const Vec3f a(m->absorption[0], m->absorption[1], m->absorption[2]);

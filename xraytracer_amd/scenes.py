@@ -79,6 +79,36 @@ class Medium:
         return d
 
 
+@dataclasses.dataclass
+class HomogeneousMedium:
+    """HomogeneousMedium{MIS, Achromatic, NoMIS}(g, a, s, box) (Src/medium.h:122-277).
+    kind: "mis" | "achromatic" | "nomis"; Achromatic takes scalar a, s (pass (a, a, a))."""
+    kind: str
+    g: float
+    absorption: tuple
+    scattering: tuple
+    box_min: tuple
+    box_max: tuple
+
+    KINDS = {"mis": abi.XRT_MEDIUM_HOMOGENEOUS_MIS, "achromatic": abi.XRT_MEDIUM_HOMOGENEOUS_ACHROMATIC,
+             "nomis": abi.XRT_MEDIUM_HOMOGENEOUS_NOMIS}
+
+    def bounds(self):
+        return (np.asarray(self.box_min, np.float32), np.asarray(self.box_max, np.float32))
+
+    def desc(self) -> abi.XrtMediumDesc:
+        d = abi.XrtMediumDesc()
+        lo, hi = self.bounds()
+        for i in range(3):
+            d.bbox_min[i] = lo[i]
+            d.bbox_max[i] = hi[i]
+            d.absorption[i] = self.absorption[i]
+            d.scattering[i] = self.scattering[i]
+        d.g = self.g
+        d.kind = self.KINDS[self.kind]
+        return d
+
+
 class SceneBundle:
     """A host Scene (C++), its flattened description, camera and optional medium."""
 
