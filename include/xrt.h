@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 6
+#define XRT_ABI_VERSION 7
 
 /* ---- status codes ---------------------------------------------------------------- */
 enum {
@@ -186,6 +186,13 @@ int  xrt_render(xrt_ctx* ctx, const xrt_render_params* p, float* rgb_out, xrt_st
  * multi-GPU caller can reduce framebuffers over RCCL without a host round trip. */
 int  xrt_render_device(xrt_ctx* ctx, const xrt_render_params* p, float* d_rgb_out, xrt_stats* st);
 
+/* Output stage: Image::gammaCorrection(gamma) then writePPM's 8-bit quantisation
+ * (Src/image.h:80-114) on the device, for n_pixels float3 pixels: d_rgb is a DEVICE
+ * pointer on this context's GPU, or NULL for the framebuffer of the last xrt_render;
+ * rgb8_out is caller-owned HOST memory of 3 * n_pixels bytes (the R G B values writePPM
+ * prints, in pixel order). */
+int  xrt_tonemap(xrt_ctx* ctx, const float* d_rgb, uint32_t n_pixels, float gamma, uint8_t* rgb8_out);
+
 /* ---- host scene layer (C facade over the C++ Scene API; no GPU needed) ------------- */
 typedef struct xrt_hscene xrt_hscene;
 xrt_hscene* xrt_hscene_create(void);
@@ -234,6 +241,8 @@ int xrt_test_trig_draw_domain(xrt_ctx* ctx, uint32_t first_bits, uint32_t count,
                               float* out_cos, float* out_r);
 /* glibc-logf/expf restatement on device over x[i]: out[2i] = logf, out[2i+1] = expf */
 int xrt_test_logexp(xrt_ctx* ctx, const float* x, uint32_t n, float* out);
+/* glibc-powf restatement on device: out[i] = powf(x[i], y) */
+int xrt_test_powf(xrt_ctx* ctx, const float* x, uint32_t n, float y, float* out);
 /* every 32-bit input: mode 0 checks the device's fast correctly rounded reciprocal against
  * 1.0f / b, mode 1 its division by the constant c (rc = 1.0f / c) against x / c; returns the
  * mismatch count and up to 16 mismatching inputs (0xffffffff = unused) */

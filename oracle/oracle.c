@@ -1088,3 +1088,19 @@ void orc_libm_sincosf(const float* x, uint32_t n, float* s, float* c) {
         c[i] = cosf(x[i]);
     }
 }
+
+/* host libm powf (checker for the device restatement) */
+void orc_libm_powf(const float* x, uint32_t n, float y, float* out) {
+    for (uint32_t i = 0; i < n; ++i) out[i] = powf(x[i], y);
+}
+
+/* Image::gammaCorrection (Src/image.h:80-90) then writePPM's per-channel value
+ * std::clamp(static_cast<uint32_t>(255.0f * c), 0u, 255u) (:92-114) over n floats */
+void orc_tonemap(const float* rgb, uint32_t n, float gamma, uint8_t* out) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const float c = powf(rgb[i], 1.0f / gamma);
+        uint32_t u = (uint32_t)(255.0f * c);
+        out[i] = (uint8_t)(u > 255u ? 255u : u);
+    }
+}
+

@@ -88,6 +88,9 @@ void orc_kat_light(orc_mt* m, const xrt_light* l, const float* pos, float* out);
 /* host libm sinf/cosf (checker for the device restatement) */
 void orc_libm_sincosf(const float* x, uint32_t n, float* s, float* c);
 void orc_libm_logexpf(const float* x, uint32_t n, float* lg, float* ex);
+void orc_libm_powf(const float* x, uint32_t n, float y, float* out);
+/* Image::gammaCorrection + writePPM quantisation (Src/image.h:80-114), n floats -> n bytes */
+void orc_tonemap(const float* rgb, uint32_t n, float gamma, uint8_t* out);
 
 #ifdef __cplusplus
 }

@@ -72,6 +72,8 @@ def lib():
         l.orc_kat_light.argtypes = [C.POINTER(OrcMT), C.POINTER(abi.XrtLight), f32p, f32p]
         l.orc_libm_sincosf.argtypes = [f32p, C.c_uint32, f32p, f32p]
         l.orc_libm_logexpf.argtypes = [f32p, C.c_uint32, f32p, f32p]
+        l.orc_libm_powf.argtypes = [f32p, C.c_uint32, C.c_float, f32p]
+        l.orc_tonemap.argtypes = [f32p, C.c_uint32, C.c_float, C.POINTER(C.c_uint8)]
         _lib = l
     return _lib
 
@@ -157,3 +159,19 @@ def libm_sincosf(x):
     c = np.empty_like(x)
     lib().orc_libm_sincosf(fp(x), len(x), fp(s), fp(c))
     return s, c
+
+
+def libm_powf(x, y):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(x)
+    lib().orc_libm_powf(fp(x), len(x), float(y), fp(out))
+    return out
+
+
+def tonemap(img, gamma):
+    """Image::gammaCorrection(gamma) + writePPM's 8-bit values, as uint8 of img's shape."""
+    a = np.ascontiguousarray(img, dtype=np.float32)
+    out = np.empty(a.shape, np.uint8)
+    lib().orc_tonemap(fp(a.reshape(-1)), a.size, float(gamma), out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return out
+

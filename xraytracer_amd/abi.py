@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(HERE, "libxrt_hip.so")
 if os.environ.get("XRT_LIB"):   # experiment builds (csrc/Makefile `variant`), same ABI
     LIB_PATH = os.path.join(HERE, os.environ["XRT_LIB"])
 
-XRT_ABI_VERSION = 6   # include/xrt.h XRT_ABI_VERSION
+XRT_ABI_VERSION = 7   # include/xrt.h XRT_ABI_VERSION
 XRT_OK = 0
 XRT_OBJ_MESH, XRT_OBJ_SPHERE, XRT_OBJ_BOX = 0, 1, 2
 XRT_LIGHT_QUAD, XRT_LIGHT_TRIANGLE, XRT_LIGHT_SPHERE = 0, 1, 2
@@ -115,6 +115,8 @@ SIGNATURES = {
     "xrt_test_trig": (C.c_int, [C.c_void_p, f32p, C.c_uint32, f32p]),
     "xrt_test_trig_draw_domain": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, f32p, f32p, f32p]),
     "xrt_test_logexp": (C.c_int, [C.c_void_p, f32p, C.c_uint32, f32p]),
+    "xrt_test_powf": (C.c_int, [C.c_void_p, f32p, C.c_uint32, C.c_float, f32p]),
+    "xrt_tonemap": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_float, C.POINTER(C.c_uint8)]),
     "xrt_test_fastdiv": (C.c_int, [C.c_void_p, C.c_uint32, C.c_float, C.c_float, C.POINTER(C.c_uint64), u32p]),
 }
 

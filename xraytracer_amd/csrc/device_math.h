@@ -254,4 +254,103 @@ __device__ __forceinline__ float glibc_expf(float x) {
     return (float)(y * s);
 }
 
+// ---- glibc powf -----------------------------------------------------------------------
+// Image::gammaCorrection's std::pow(float, float) (Src/image.h:80-90).  Restatement of
+// glibc 2.35 e_powf.c (ARM optimized-routines) as the x86-64 FMA ifunc variant executes it:
+// log2 of x in double from __powf_log2_data (16-entry table + order-5 polynomial, the
+// table identical to __log2f_data's), y * log2(x), then exp2 from __exp2f_data (tab,
+// shift_scaled, unscaled poly); tables read from the host libm.so.6.  Special cases
+// (zero / inf / nan, negative x with integer y, subnormal x) follow the published code.
+// Checked bit-for-bit against host powf (tests/test_gpu_parity.py, xrt_test_powf).
+static __constant__ const double kPowfLog2Tab[16][2] = {
+    {0x1.661ec79f8f3bep+0, -0x1.efec65b963019p-2}, {0x1.571ed4aaf883dp+0, -0x1.b0b6832d4fca4p-2},
+    {0x1.49539f0f010b0p+0, -0x1.7418b0a1fb77bp-2}, {0x1.3c995b0b80385p+0, -0x1.39de91a6dcf7bp-2},
+    {0x1.30d190c8864a5p+0, -0x1.01d9bf3f2b631p-2}, {0x1.25e227b0b8ea0p+0, -0x1.97c1d1b3b7af0p-3},
+    {0x1.1bb4a4a1a343fp+0, -0x1.2f9e393af3c9fp-3}, {0x1.12358f08ae5bap+0, -0x1.960cbbf788d5cp-4},
+    {0x1.0953f419900a7p+0, -0x1.a6f9db6475fcep-5}, {0x1.0000000000000p+0, 0x0.0p+0},
+    {0x1.e608cfd9a47acp-1, 0x1.338ca9f24f53dp-4}, {0x1.ca4b31f026aa0p-1, 0x1.476a9543891bap-3},
+    {0x1.b2036576afce6p-1, 0x1.e840b4ac4e4d2p-3}, {0x1.9c2d163a1aa2dp-1, 0x1.40645f0c6651cp-2},
+    {0x1.886e6037841edp-1, 0x1.88e9c2c1b9ff8p-2}, {0x1.767dcf5534862p-1, 0x1.ce0a44eb17bccp-2}};
+__device__ __forceinline__ bool powf_zeroinfnan(uint32_t i) { return 2u * i - 1u >= 2u * 0x7f800000u - 1u; }
+// 0: not an integer, 1: odd integer, 2: even integer (checkint)
+__device__ __forceinline__ int powf_checkint(uint32_t iy) {
+    const int e = (int)(iy >> 23 & 0xff);
+    if (e < 0x7f) return 0;
+    if (e > 0x7f + 23) return 2;
+    if (iy & ((1u << (0x7f + 23 - e)) - 1u)) return 0;
+    if (iy & (1u << (0x7f + 23 - e))) return 1;
+    return 2;
+}
+__device__ __forceinline__ float glibc_powf(float x, float y) {
+    const double A0 = 0x1.27616c9496e0bp-2, A1 = -0x1.71969a075c67ap-2, A2 = 0x1.ec70a6ca7baddp-2,
+                 A3 = -0x1.7154748bef6c8p-1, A4 = 0x1.71547652ab82bp+0;
+    const double SHIFT = 0x1.8p+47, C0 = 0x1.c6af84b912394p-5, C1 = 0x1.ebfce50fac4f3p-3,
+                 C2 = 0x1.62e42ff0c52d6p-1;
+    uint32_t sign_bias = 0;
+    uint32_t ix = __float_as_uint(x);
+    const uint32_t iy = __float_as_uint(y);
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u || powf_zeroinfnan(iy)) {
+        if (powf_zeroinfnan(iy)) {
+            if (2u * iy == 0u) return 1.0f;   // signalling-NaN x aside
+            if (ix == 0x3f800000u) return 1.0f;
+            if (2u * ix > 2u * 0x7f800000u || 2u * iy > 2u * 0x7f800000u) return x + y;
+            if (2u * ix == 2u * 0x3f800000u) return 1.0f;
+            if ((2u * ix < 2u * 0x3f800000u) == !(iy & 0x80000000u)) return 0.0f;
+            return y * y;
+        }
+        if (powf_zeroinfnan(ix)) {
+            float x2 = x * x;
+            if ((ix & 0x80000000u) && powf_checkint(iy) == 1) x2 = -x2;
+            return (iy & 0x80000000u) ? 1.0f / x2 : x2;
+        }
+        if (ix & 0x80000000u) {   // finite x < 0
+            const int yint = powf_checkint(iy);
+            if (yint == 0) return __builtin_nanf("");
+            if (yint == 1) sign_bias = 1u << (5 + 11);
+            ix &= 0x7fffffffu;
+        }
+        if (ix < 0x00800000u) {   // subnormal x
+            ix = __float_as_uint(__uint_as_float(ix) * 0x1p23f);
+            ix &= 0x7fffffffu;
+            ix -= 23u << 23;
+        }
+    }
+    // log2_inline
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int i = (int)((tmp >> (23 - 4)) % 16);
+    const uint32_t top = tmp & 0xff800000u;
+    const uint32_t iz = ix - top;
+    const int k = (int32_t)top >> 23;
+    const double invc = kPowfLog2Tab[i][0], logc = kPowfLog2Tab[i][1];
+    const double z = (double)__uint_as_float(iz);
+    const double r = __builtin_fma(z, invc, -1.0);
+    const double y0 = logc + (double)k;
+    const double r2 = r * r;
+    double yy = __builtin_fma(A0, r, A1);
+    const double p = __builtin_fma(A2, r, A3);
+    const double r4 = r2 * r2;
+    double q = __builtin_fma(A4, r, y0);
+    q = __builtin_fma(p, r2, q);
+    yy = __builtin_fma(yy, r4, q);
+    const double ylogx = (double)y * yy;
+    if (((uint64_t)__double_as_longlong(ylogx) >> 47 & 0xffff) >= ((uint64_t)__double_as_longlong(126.0) >> 47)) {
+        if (ylogx > 0x1.fffffffd1d571p+6) return sign_bias ? -__builtin_inff() : __builtin_inff();
+        if (ylogx <= -150.0) return sign_bias ? -0.0f : 0.0f;
+    }
+    // exp2_inline
+    double kd = ylogx + SHIFT;
+    const uint64_t ki = (uint64_t)__double_as_longlong(kd);
+    kd -= SHIFT;
+    const double rr = ylogx - kd;
+    uint64_t t = kExp2fTab[ki % 32];
+    const uint64_t ski = ki + sign_bias;
+    t += ski << (52 - 5);
+    const double s = __longlong_as_double((long long)t);
+    const double zz = __builtin_fma(C0, rr, C1);
+    const double rr2 = rr * rr;
+    double e = __builtin_fma(C2, rr, 1.0);
+    e = __builtin_fma(zz, rr2, e);
+    return (float)(e * s);
+}
+
 }  // namespace xrt

@@ -45,6 +45,9 @@ hipError_t launch_test_rng(const uint32_t* seeds, uint32_t n_seeds, uint32_t ski
 hipError_t launch_test_trig(const float* x, uint32_t n, float* out, hipStream_t st);
 hipError_t launch_test_trig_domain(uint32_t first, uint32_t count, float* s, float* c, float* r, hipStream_t st);
 hipError_t launch_test_logexp(const float* x, uint32_t n, float* out, hipStream_t st);
+hipError_t launch_test_powf(const float* x, uint32_t n, float y, float* out, hipStream_t st);
+// Image::gammaCorrection + writePPM quantisation of n floats into n bytes
+hipError_t launch_tonemap(const float* rgb, uint32_t n, float inv_gamma, uint8_t* out, hipStream_t st);
 hipError_t launch_test_fastdiv(uint32_t mode, float c, float rc, uint32_t first, uint32_t count,
                                unsigned long long* nbad, uint32_t* bad, hipStream_t st);
 }  // namespace xrt

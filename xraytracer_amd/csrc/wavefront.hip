@@ -2087,6 +2087,25 @@ __global__ void k_test_logexp(const float* x, uint32_t n, float* out) {
     }
 }
 
+__global__ void k_test_powf(const float* x, uint32_t n, float y, float* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = glibc_powf(x[i], y);
+}
+
+// ===================================================================== output ====
+// Image::gammaCorrection (Src/image.h:80-90: pow(c, 1.0f / gamma) per channel) followed by
+// writePPM's quantisation (:92-114: std::clamp(static_cast<uint32_t>(255.0f * c), 0u, 255u)),
+// the float -> uint32 conversion as GCC emits it on x86-64 (a 64-bit truncating convert,
+// INT64_MIN for NaN and out-of-range values, low 32 bits kept).  One thread per channel.
+__global__ void k_tonemap(const float* __restrict__ rgb, uint32_t n, float inv_gamma, uint8_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float v = 255.0f * glibc_powf(rgb[i], inv_gamma);
+    const int64_t q = (v >= -0x1p63f && v < 0x1p63f) ? (int64_t)v : INT64_MIN;
+    const uint32_t u = (uint32_t)(uint64_t)q;
+    out[i] = (uint8_t)(u < 255u ? u : 255u);
+}
+
 // ================================================================== launchers ====
 }  // namespace xrt
 
@@ -2268,6 +2287,16 @@ hipError_t launch_test_fastdiv(uint32_t mode, float c, float rc, uint32_t first,
 
 hipError_t launch_test_logexp(const float* x, uint32_t n, float* out, hipStream_t st) {
     hipLaunchKernelGGL(k_test_logexp, dim3((n + 255) / 256), dim3(256), 0, st, x, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_test_powf(const float* x, uint32_t n, float y, float* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_test_powf, dim3((n + 255) / 256), dim3(256), 0, st, x, n, y, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_tonemap(const float* rgb, uint32_t n, float inv_gamma, uint8_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_tonemap, dim3((n + 255) / 256), dim3(256), 0, st, rgb, n, inv_gamma, out);
     return hipGetLastError();
 }
 

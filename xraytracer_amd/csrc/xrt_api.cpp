@@ -752,6 +752,37 @@ int xrt_test_logexp(xrt_ctx* c, const float* x, uint32_t n, float* out) {
     return e == hipSuccess ? XRT_OK : hip_err(c, e, "xrt_test_logexp");
 }
 
+int xrt_test_powf(xrt_ctx* c, const float* x, uint32_t n, float y, float* out) {
+    if (!c || !x || !out) return XRT_ERR_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    DevBuf dx, dout;
+    int rc;
+    if ((rc = ensure(c, dx, (size_t)n * 4 + 16)) || (rc = ensure(c, dout, (size_t)n * 4 + 16))) return rc;
+    hipError_t e = hipMemcpy(dx.p, x, (size_t)n * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_test_powf(as<float>(dx), n, y, as<float>(dout), c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, dout.p, (size_t)n * 4, hipMemcpyDeviceToHost);
+    free_buf(dx), free_buf(dout);
+    return e == hipSuccess ? XRT_OK : hip_err(c, e, "xrt_test_powf");
+}
+
+int xrt_tonemap(xrt_ctx* c, const float* d_rgb, uint32_t n_pixels, float gamma, uint8_t* rgb8_out) {
+    if (!c || !rgb8_out) return XRT_ERR_INVALID;
+    const float* src = d_rgb ? d_rgb : as<float>(c->fb);
+    if (!src || (!d_rgb && (size_t)n_pixels * 3 * sizeof(float) > c->fb.bytes))
+        return set_err(c, XRT_ERR_STATE, "xrt_tonemap: no framebuffer of that size (render first)");
+    HIPCHK(c, hipSetDevice(c->device));
+    DevBuf out;
+    int rc;
+    const size_t n = (size_t)n_pixels * 3;
+    if ((rc = ensure(c, out, n + 16))) return rc;
+    hipError_t e = launch_tonemap(src, (uint32_t)n, 1.0f / gamma, as<uint8_t>(out), c->stream);   // Src/image.h:85
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(rgb8_out, out.p, n, hipMemcpyDeviceToHost);
+    free_buf(out);
+    return e == hipSuccess ? XRT_OK : hip_err(c, e, "xrt_tonemap");
+}
+
 int xrt_test_trig_draw_domain(xrt_ctx* c, uint32_t first, uint32_t count, float* out_sin, float* out_cos, float* out_r) {
     if (!c || !out_sin || !out_cos || !out_r) return XRT_ERR_INVALID;
     HIPCHK(c, hipSetDevice(c->device));

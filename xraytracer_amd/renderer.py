@@ -78,6 +78,23 @@ class HipRenderer:
         self.stats = st
         return img
 
+    def tonemap(self, width: int, height: int, gamma: float, device_ptr: int = 0) -> np.ndarray:
+        """Image::gammaCorrection(gamma) + writePPM's 8-bit quantisation on the GPU, of the
+        last render() (device_ptr 0) or of a device float3 buffer: (H, W, 3) uint8."""
+        out = np.empty((height, width, 3), np.uint8)
+        self._check(self._lib.xrt_tonemap(self.ctx, C.c_void_p(device_ptr or None), width * height, C.c_float(gamma),
+                                          out.ctypes.data_as(C.POINTER(C.c_uint8))), "xrt_tonemap")
+        return out
+
+    @staticmethod
+    def write_ppm(path: str, rgb8: np.ndarray):
+        """Image::writePPM's text format (Src/image.h:92-114): P3, width height, 255, one
+        "R G B" line per pixel."""
+        h, w, _ = rgb8.shape
+        with open(path, "w") as f:
+            f.write(f"P3\n{w} {h}\n255\n")
+            f.write("".join(f"{r} {g} {b}\n" for r, g, b in rgb8.reshape(-1, 3).tolist()))
+
     def render_device(self, scene: SceneBundle, width: int, height: int, out_ptr: int, **kw):
         """Render into a device buffer (e.g. torch tensor .data_ptr()) of H*W*3 float32."""
         if self._uploaded is not scene:
