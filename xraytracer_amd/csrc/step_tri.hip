@@ -625,15 +625,39 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
 // --------------------------------------------------------------- RNG refills ----
 // k_refill_merged: the merged schedule's ring refill.  Same twist as wave_twist (libstdc++
 // _M_gen_rand: x[g+k] = x[g+k-227] ^ mix(x[g+k-624], x[g+k-623]), chunks k = m, 227+m,
-// 454+m held in registers), arranged for bandwidth: every load of a twist is issued before
-// the first use (clamped indices instead of guarded loads), the next request's slot and
-// stream position are fetched while the current one twists, and the slot state is not
-// touched — the merged kernel clears ST_RNGREQ when it next loads the slot, which is always
-// after this kernel (one refill launch follows every step launch).
-__device__ __forceinline__ void twist_block(uint32_t* ring, uint32_t g, int lane) {
-    const uint32_t h = g % kRing;
-    gu32* old = glb<gu32>(ring + (kMT - h));
-    uint32_t* nw = ring + h;
+// 454+m held in registers), arranged for bandwidth: the old block is staged through LDS
+// (below), the next request's slot, stream position and old block are fetched while the
+// current one twists, and the slot state is not touched — the merged kernel clears
+// ST_RNGREQ when it next loads the slot, which is always after this kernel (one refill
+// launch follows every step launch).
+// One twist of a slot's ring by a whole wave, staged through LDS: the old block (624 words,
+// 16-byte aligned because kRing*4 and kMT*4 are multiples of 16) comes in as 156 dwordx4
+// loads (3 instructions per wave) and every recurrence operand is then an LDS read, instead
+// of 26 overlapping global_load_dword per lane whose 64-lane requests re-fetch each cache
+// line ~2.6 times through the TA.  The new words go out as 11 coalesced dword stores.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+struct Staged { u32x4 v[3]; };
+
+__device__ __forceinline__ Staged load_block(const uint32_t* ring, uint32_t g, int lane) {
+    const u32x4* old = reinterpret_cast<const u32x4*>(ring + (kMT - g % kRing));
+    Staged r;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        r.v[k] = __builtin_nontemporal_load(old + min((uint32_t)lane + 64u * k, (uint32_t)(kMT / 4 - 1)));
+    return r;
+}
+
+__device__ __forceinline__ void store_block(const Staged& r, int lane, uint32_t* lds) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t q = (uint32_t)lane + 64u * k;
+        if (q < kMT / 4) reinterpret_cast<u32x4*>(lds)[q] = r.v[k];
+    }
+    wave_sync();
+}
+
+__device__ __forceinline__ void twist_block(uint32_t* ring, uint32_t g, int lane, const uint32_t* old) {
+    uint32_t* nw = ring + g % kRing;
     uint32_t x0[4], x1[4], x397[4], y0[4], y1[4], z0[3], z1[3];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -666,6 +690,7 @@ __device__ __forceinline__ void twist_block(uint32_t* ring, uint32_t g, int lane
 
 __global__ __launch_bounds__(kBlock) void k_refill_merged(KParams P, const uint32_t* __restrict__ req,
                                                           const uint32_t* __restrict__ count, uint32_t* zero_count) {
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kBlock / 64][2][kMT];
     zero_parts(P, zero_count);
     const PartIter it = part_iter(P, count, kBlock / 64);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -674,19 +699,31 @@ __global__ __launch_bounds__(kBlock) void k_refill_merged(KParams P, const uint3
     const uint32_t* rq = req + it.p * P.part_cap;
     uint32_t s = rq[i];
     uint32_t g = glb<gu32>(P.rng_g)[s];
-    while (true) {
+    store_block(load_block(P.ring + (size_t)s * kRing, g, lane), lane, stage[wv][0]);
+    for (int buf = 0;; buf ^= 1) {
+        // Double-buffered: the next request's old block is in flight (in registers) while
+        // this one twists out of LDS.
         const uint32_t in = i + it.stride;
-        const uint32_t sn = in < it.n ? rq[in] : s;
-        twist_block(P.ring + (size_t)s * kRing, g, lane);
+        const bool more = in < it.n;
+        uint32_t sn = s, gn = g;
+        Staged nx;
+        if (more) {
+            sn = rq[in];
+            gn = glb<gu32>(P.rng_g)[sn];
+            nx = load_block(P.ring + (size_t)sn * kRing, gn, lane);
+        }
+        twist_block(P.ring + (size_t)s * kRing, g, lane, stage[wv][buf]);
         if (lane == 0) P.rng_g[s] = g + kMT;
-        if (in >= it.n) break;
-        g = glb<gu32>(P.rng_g)[sn];
-        s = sn, i = in;
+        if (!more) break;
+        store_block(nx, lane, stage[wv][buf ^ 1]);
+        s = sn, g = gn, i = in;
     }
 }
 
 hipError_t launch_refill_merged(const KParams& P, const uint32_t* count, uint32_t* zero_count, hipStream_t st) {
-    const uint32_t per = std::max<uint32_t>(1u, std::min<uint32_t>((P.part_cap + 3) / 4, 4096u / P.n_part));
+    // 16384 blocks (64 Ki waves) measured best on C2: 2048 7.7 ms, 4096 6.9, 8192 6.6, 16384 6.5
+    // per frame (tools/refill_sweep.sh).
+    const uint32_t per = std::max<uint32_t>(1u, std::min<uint32_t>((P.part_cap + 3) / 4, 16384u / P.n_part));
     hipLaunchKernelGGL(k_refill_merged, dim3(P.n_part * per), dim3(kBlock), 0, st, P, P.req, count, zero_count);
     return hipGetLastError();
 }
