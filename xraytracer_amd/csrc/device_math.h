@@ -132,49 +132,46 @@ __device__ __forceinline__ double sincosf_reduce(double x, int& n) {
     n = (((int32_t)r) + 0x800000) >> 24;
     return x - n * kSC_hpi;
 }
-// sincosf_poly(x * sign[n & 3], x * x, table (n & 2) ? 1 : 0, n) for quadrant n
-__device__ __forceinline__ float sincosf_quadrant(double x, int n) {
-    if ((n & 1) == 0) {
-        const double sg = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;   // sign[n & 3] (n even: 1 or -1)
-        return sincosf_sin_poly(x * sg, x * x);
+// sinf and cosf of one argument together, without divergence.  glibc evaluates, per call,
+// sincosf_poly(x * sign[n & 3], x * x, table (n & 2), n) for sinf and the same with n ^ 1
+// for cosf, where n even takes the sine polynomial and n odd the cosine one; so for any n
+// one of the two results is the sine polynomial and the other the cosine polynomial of the
+// same reduced x, and each is evaluated once here, then placed by selects:
+//  * the sine polynomial is odd and IEEE negation commutes exactly with * and + (and with
+//    the cast to float), so sin_poly(x * sign) == sign * sin_poly(x) bit for bit;
+//  * sign[n & 3] = {1, -1, -1, 1}: sinf (n even) takes -sp iff n & 2, cosf (n odd) iff !(n & 2);
+//  * both cosine branches negate iff n & 2 (second coefficient set = negated first);
+//  * glibc's |y| < pi/4 path skips the reduction: there it yields n == 0 and x - 0 * hpi ==
+//    x exactly (|y| * 2/pi * 2^23 < 2^22), so the reduced evaluation is the same numbers;
+//  * |y| < 2^-12: sinf returns y, cosf 1.0f.
+__device__ __forceinline__ void glibc_sincosf(float y, float& so, float& co) {
+    const uint32_t top = abstop12(y);
+    if (top >= abstop12(120.0f)) {   // |y| >= 120 or NaN/Inf: outside every sampled domain
+        so = __builtin_sinf(y), co = __builtin_cosf(y);
+        return;
     }
-    const double c = sincosf_cos_poly(x * x);
-    return (float)((n & 2) ? -c : c);
+    int n;
+    const double x = sincosf_reduce((double)y, n);
+    const double x2 = x * x;
+    const float sp = sincosf_sin_poly(x, x2);
+    const double cp = sincosf_cos_poly(x2);
+    const bool odd = (n & 1) != 0, neg2 = (n & 2) != 0;
+    const float cf = (float)(neg2 ? -cp : cp);
+    const float s_even = neg2 ? -sp : sp;   // sinf, n even
+    const float c_odd = neg2 ? sp : -sp;    // cosf, n odd
+    const bool tiny = top < abstop12(0x1p-12f);
+    so = tiny ? y : (odd ? cf : s_even);
+    co = tiny ? 1.0f : (odd ? c_odd : cf);
 }
 __device__ __forceinline__ float glibc_sinf(float y) {
-    const float pio4f = 0x1.921FB6p-1f;
-    double x = y;
-    if (abstop12(y) < abstop12(pio4f)) {
-        if (abstop12(y) < abstop12(0x1p-12f)) return y;
-        return sincosf_sin_poly(x, x * x);
-    }
-    if (abstop12(y) < abstop12(120.0f)) {
-        int n;
-        x = sincosf_reduce(x, n);
-        return sincosf_quadrant(x, n);
-    }
-    return __builtin_sinf(y);  // |x| >= 120: outside every domain this renderer samples
+    float s, c;
+    glibc_sincosf(y, s, c);
+    return s;
 }
 __device__ __forceinline__ float glibc_cosf(float y) {
-    const float pio4f = 0x1.921FB6p-1f;
-    double x = y;
-    if (abstop12(y) < abstop12(pio4f)) {
-        if (abstop12(y) < abstop12(0x1p-12f)) return 1.0f;
-        return (float)sincosf_cos_poly(x * x);
-    }
-    if (abstop12(y) < abstop12(120.0f)) {
-        int n;
-        x = sincosf_reduce(x, n);
-        // glibc: sincosf_poly(x * sign[n & 3], x * x, table (n & 2), n ^ 1): the sine branch
-        // takes the sign of quadrant n, the cosine branch the table of quadrant n
-        if (((n ^ 1) & 1) == 0) {
-            const double sg = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;
-            return sincosf_sin_poly(x * sg, x * x);
-        }
-        const double c = sincosf_cos_poly(x * x);
-        return (float)((n & 2) ? -c : c);
-    }
-    return __builtin_cosf(y);
+    float s, c;
+    glibc_sincosf(y, s, c);
+    return c;
 }
 
 // ---- glibc logf / expf ----------------------------------------------------------------

@@ -323,7 +323,9 @@ __device__ inline v3 light_sample(const DLight& L, v3 x, v3& wi, float& pdf, flo
         sin_theta_2 / sin_theta_max + cos_theta * __builtin_sqrtf(smax(0.0f, 1.0f - sin_theta_2 / sin_theta_max_2));
     const float sin_alpha = __builtin_sqrtf(smax(0.0f, 1.0f - cos_alpha * cos_alpha));
     const float phi = kPI_MUL_2 * rng.next();
-    const v3 nn = (dx * (glibc_cosf(phi) * sin_alpha) + dy * (glibc_sinf(phi) * sin_alpha)) + dz * cos_alpha;
+    float sphi, cphi;
+    glibc_sincosf(phi, sphi, cphi);
+    const v3 nn = (dx * (cphi * sin_alpha) + dy * (sphi * sin_alpha)) + dz * cos_alpha;
     const v3 p = center + nn * radius;
     const v3 dd = p - x;
     tmax = length(dd);
@@ -340,8 +342,10 @@ __device__ __forceinline__ v3 lambert_sample_f(v3 ng, v3 dpdu, v3 dpdv, RNG& rng
     const float r2 = rng.next();
     const float sinTheta = __builtin_sqrtf(1.0f - r1 * r1);
     const float phi = 2.0f * kPI * r2;
-    const float x = sinTheta * glibc_cosf(phi);
-    const float z = sinTheta * glibc_sinf(phi);
+    float sphi, cphi;
+    glibc_sincosf(phi, sphi, cphi);
+    const float x = sinTheta * cphi;
+    const float z = sinTheta * sphi;
     return local_to_world(mk(x, r1, z), dpdu, ng, dpdv);
 }
 __device__ __forceinline__ v3 lambert_sample(const Surf& S, Rng& rng) {
@@ -349,8 +353,10 @@ __device__ __forceinline__ v3 lambert_sample(const Surf& S, Rng& rng) {
     const float r2 = rng.next();
     const float sinTheta = __builtin_sqrtf(1.0f - r1 * r1);
     const float phi = 2.0f * kPI * r2;
-    const float x = sinTheta * glibc_cosf(phi);
-    const float z = sinTheta * glibc_sinf(phi);
+    float sphi, cphi;
+    glibc_sincosf(phi, sphi, cphi);
+    const float x = sinTheta * cphi;
+    const float z = sinTheta * sphi;
     return local_to_world(mk(x, r1, z), S.dpdu, S.ng, S.dpdv);
 }
 

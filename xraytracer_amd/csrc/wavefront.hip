@@ -485,7 +485,9 @@ __device__ void hg_sample(float g, v3 wo, Rng& rng, v3& wi) {
     }
     const float sinTheta = __builtin_sqrtf(smax(1.0f - cosTheta * cosTheta, 0.0f));
     const float phi = 2.0f * kPI * u1;
-    const v3 wl = mk(glibc_cosf(phi) * sinTheta, cosTheta, glibc_sinf(phi) * sinTheta);
+    float sphi, cphi;
+    glibc_sincosf(phi, sphi, cphi);
+    const v3 wl = mk(cphi * sinTheta, cosTheta, sphi * sinTheta);
     v3 t, b;
     onb(wo, t, b);
     wi = local_to_world(wl, t, wo, b);
