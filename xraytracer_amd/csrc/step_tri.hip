@@ -656,8 +656,11 @@ __device__ __forceinline__ void store_block(const Staged& r, int lane, uint32_t*
     wave_sync();
 }
 
-__device__ __forceinline__ void twist_block(uint32_t* ring, uint32_t g, int lane, const uint32_t* old) {
-    uint32_t* nw = ring + g % kRing;
+// The new block goes back out through the same LDS buffer (its old words are all in
+// registers by then) as 156 dwordx4 stores: whole 64-byte runs instead of 11 dword stores
+// per lane that start at arbitrary offsets within a cache line.
+__device__ __forceinline__ void twist_block(uint32_t* ring, uint32_t g, int lane, uint32_t* buf) {
+    const uint32_t* old = buf;
     uint32_t x0[4], x1[4], x397[4], y0[4], y1[4], z0[3], z1[3];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -676,15 +679,23 @@ __device__ __forceinline__ void twist_block(uint32_t* ring, uint32_t g, int lane
     const uint32_t n0 = __builtin_amdgcn_readfirstlane(a[0]);   // x[g]: the new block's first word
 #pragma unroll
     for (int j = 0; j < 4; ++j) b[j] = a[j] ^ mt_mix(y0[j], y1[j]);
+    wave_sync();   // every old word is in registers before the buffer is overwritten
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         const uint32_t m = (uint32_t)lane + 64u * j;
-        if (m < 170u) nw[454 + m] = b[j] ^ mt_mix(z0[j], m + 455 < kMT ? z1[j] : n0);
+        if (m < 170u) buf[454 + m] = b[j] ^ mt_mix(z0[j], m + 455 < kMT ? z1[j] : n0);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint32_t m = (uint32_t)lane + 64u * j;
-        if (m < 227u) nw[m] = a[j], nw[227 + m] = b[j];
+        if (m < 227u) buf[m] = a[j], buf[227 + m] = b[j];
+    }
+    wave_sync();
+    u32x4* nw = reinterpret_cast<u32x4*>(ring + g % kRing);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t q = (uint32_t)lane + 64u * k;
+        if (q < kMT / 4) nw[q] = reinterpret_cast<const u32x4*>(buf)[q];
     }
 }
 
