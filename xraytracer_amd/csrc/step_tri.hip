@@ -69,13 +69,34 @@ struct RngRegs {
             i = (i + 1 == kRing) ? 0u : i + 1;
         }
     }
+    // NW consecutive words in ceil(NW / 4) vector loads (dword-aligned dwordx4 / dwordx2:
+    // a quarter of the address work of NW dword loads); a lane whose window wraps past the
+    // ring's end takes dword loads
     __device__ __forceinline__ void prefetch(const uint32_t* ring) {
-        gu32* r = glb<gu32>(ring);
-        uint32_t i = c % kRing;
+        typedef uint32_t u4u __attribute__((ext_vector_type(4), aligned(4)));
+        typedef uint32_t u2u __attribute__((ext_vector_type(2), aligned(4)));
+        using gu4 = __attribute__((address_space(1))) const u4u;
+        using gu2 = __attribute__((address_space(1))) const u2u;
+        static_assert(NW % 2 == 0, "even window");
+        const uint32_t i = c % kRing;
+        if (i <= kRing - NW) {
 #pragma unroll
-        for (int j = 0; j < NW; ++j) {
-            pf[j] = r[i];
-            i = (i + 1 == kRing) ? 0u : i + 1;
+            for (int j = 0; j + 4 <= NW; j += 4) {
+                const u4u v = *(gu4*)(ring + i + j);
+                pf[j] = v.x, pf[j + 1] = v.y, pf[j + 2] = v.z, pf[j + 3] = v.w;
+            }
+            if constexpr (NW % 4 == 2) {
+                const u2u v = *(gu2*)(ring + i + NW - 2);
+                pf[NW - 2] = v.x, pf[NW - 1] = v.y;
+            }
+        } else {
+            gu32* r = glb<gu32>(ring);
+            uint32_t k = i;
+#pragma unroll
+            for (int j = 0; j < NW; ++j) {
+                pf[j] = r[k];
+                k = (k + 1 == kRing) ? 0u : k + 1;
+            }
         }
     }
     __device__ __forceinline__ void take() {
