@@ -34,27 +34,34 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
 }
 
 // A slot's stream: ring words x[c], x[c+1], ...  prefetch() issues the loads of the next 8
-// words at once (one memory latency for a whole shade pass instead of one per draw);
-// draws beyond the prefetched words are loaded on demand.
+// words at once (one memory latency for a whole shade pass instead of one per draw); a
+// draw past them loads the next 8 again (long delta-tracking walks: one latency per 8
+// draws, not per draw).  Words at or past the slot's generated end g may be loaded but are
+// never drawn: every caller checks g - c before drawing, exactly as for single loads.
+// Global (not flat) loads, so LDS waits do not also wait for them.
 struct Rng {
     const uint32_t* ring;
     uint32_t c;
     uint32_t nb = 0;
     uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0, b4 = 0, b5 = 0, b6 = 0, b7 = 0;
+    __device__ __forceinline__ void load8() {
+        using g32 = __attribute__((address_space(1))) const uint32_t;
+        g32* r = (g32*)ring;
+        b0 = r[c % kRing], b1 = r[(c + 1) % kRing], b2 = r[(c + 2) % kRing], b3 = r[(c + 3) % kRing];
+        b4 = r[(c + 4) % kRing], b5 = r[(c + 5) % kRing], b6 = r[(c + 6) % kRing], b7 = r[(c + 7) % kRing];
+    }
     __device__ __forceinline__ void prefetch(uint32_t avail) {
         nb = avail < 8u ? avail : 8u;
-        b0 = ring[c % kRing], b1 = ring[(c + 1) % kRing], b2 = ring[(c + 2) % kRing], b3 = ring[(c + 3) % kRing];
-        b4 = ring[(c + 4) % kRing], b5 = ring[(c + 5) % kRing], b6 = ring[(c + 6) % kRing], b7 = ring[(c + 7) % kRing];
+        load8();
     }
     __device__ __forceinline__ float next() {
-        uint32_t y;
-        if (nb) {
-            y = b0;
-            b0 = b1, b1 = b2, b2 = b3, b3 = b4, b4 = b5, b5 = b6, b6 = b7;
-            --nb;
-        } else {
-            y = ring[c % kRing];
+        if (!nb) {
+            load8();
+            nb = 8;
         }
+        const uint32_t y = b0;
+        b0 = b1, b1 = b2, b2 = b3, b3 = b4, b4 = b5, b5 = b6, b6 = b7;
+        --nb;
         ++c;
         return canonical(mt_temper(y));
     }
