@@ -44,11 +44,19 @@ struct Rng {
     uint32_t c;
     uint32_t nb = 0;
     uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0, b4 = 0, b5 = 0, b6 = 0, b7 = 0;
-    __device__ __forceinline__ void load8() {
+    __device__ __forceinline__ void load8() {   // two dword-aligned dwordx4 unless the window wraps
+        typedef uint32_t u4u __attribute__((ext_vector_type(4), aligned(4)));
+        using g4 = __attribute__((address_space(1))) const u4u;
         using g32 = __attribute__((address_space(1))) const uint32_t;
-        g32* r = (g32*)ring;
-        b0 = r[c % kRing], b1 = r[(c + 1) % kRing], b2 = r[(c + 2) % kRing], b3 = r[(c + 3) % kRing];
-        b4 = r[(c + 4) % kRing], b5 = r[(c + 5) % kRing], b6 = r[(c + 6) % kRing], b7 = r[(c + 7) % kRing];
+        const uint32_t i = c % kRing;
+        if (i <= kRing - 8) {
+            const u4u lo = *(g4*)(ring + i), hi = *(g4*)(ring + i + 4);
+            b0 = lo.x, b1 = lo.y, b2 = lo.z, b3 = lo.w, b4 = hi.x, b5 = hi.y, b6 = hi.z, b7 = hi.w;
+        } else {
+            g32* r = (g32*)ring;
+            b0 = r[i], b1 = r[(i + 1) % kRing], b2 = r[(i + 2) % kRing], b3 = r[(i + 3) % kRing];
+            b4 = r[(i + 4) % kRing], b5 = r[(i + 5) % kRing], b6 = r[(i + 6) % kRing], b7 = r[(i + 7) % kRing];
+        }
     }
     __device__ __forceinline__ void prefetch(uint32_t avail) {
         nb = avail < 8u ? avail : 8u;
