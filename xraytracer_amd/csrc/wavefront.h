@@ -120,6 +120,7 @@ struct DMedium {
     float majorant, inv_majorant;
     int kind;              // XRT_MEDIUM_* (0 heterogeneous: delta / ratio tracking)
     float sigma_t[3];      // homogeneous kinds: sigma_a + sigma_s (HomogeneousMedium ctor)
+    double inv_voxel;      // 1.0 / (double)voxel_size, once on the host (same IEEE quotient)
 };
 
 #ifdef __HIPCC__

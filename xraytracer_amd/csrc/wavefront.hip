@@ -432,17 +432,28 @@ __device__ __forceinline__ float grid_value(const DMedium& M, int i, int j, int 
 }
 __device__ __forceinline__ float vdb_lerp(float a, float b, double w) { return a + (float)((double)(b - a) * w); }
 __device__ float medium_density(const DMedium& M, v3 p) {
-    const double inv = 1.0 / (double)M.voxel_size;
+    const double inv = M.inv_voxel;
     const double xi = ((double)p.x - (double)M.origin[0]) * inv;
     const double yi = ((double)p.y - (double)M.origin[1]) * inv;
     const double zi = ((double)p.z - (double)M.origin[2]) * inv;
     const double fx = __builtin_floor(xi), fy = __builtin_floor(yi), fz = __builtin_floor(zi);
     const int i = (int)fx, j = (int)fy, k = (int)fz;
     const double u = xi - fx, v = yi - fy, w = zi - fz;
-    const float d000 = grid_value(M, i, j, k), d001 = grid_value(M, i, j, k + 1);
-    const float d010 = grid_value(M, i, j + 1, k), d011 = grid_value(M, i, j + 1, k + 1);
-    const float d100 = grid_value(M, i + 1, j, k), d101 = grid_value(M, i + 1, j, k + 1);
-    const float d110 = grid_value(M, i + 1, j + 1, k), d111 = grid_value(M, i + 1, j + 1, k + 1);
+    float d000, d001, d010, d011, d100, d101, d110, d111;
+    if (i >= 0 && j >= 0 && k >= 0 && i + 1 < M.nx && j + 1 < M.ny && k + 1 < M.nz) {
+        // interior cell: the x-neighbours are adjacent words, four dword-aligned dwordx2 loads
+        typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+        using g2 = __attribute__((address_space(1))) const f2u;
+        const float* b = M.density + ((size_t)k * M.ny + (size_t)j) * M.nx + (size_t)i;
+        const size_t sy = (size_t)M.nx, sz = (size_t)M.nx * M.ny;
+        const f2u a = *(g2*)b, c = *(g2*)(b + sz), e = *(g2*)(b + sy), f = *(g2*)(b + sy + sz);
+        d000 = a.x, d100 = a.y, d001 = c.x, d101 = c.y, d010 = e.x, d110 = e.y, d011 = f.x, d111 = f.y;
+    } else {
+        d000 = grid_value(M, i, j, k), d001 = grid_value(M, i, j, k + 1);
+        d010 = grid_value(M, i, j + 1, k), d011 = grid_value(M, i, j + 1, k + 1);
+        d100 = grid_value(M, i + 1, j, k), d101 = grid_value(M, i + 1, j, k + 1);
+        d110 = grid_value(M, i + 1, j + 1, k), d111 = grid_value(M, i + 1, j + 1, k + 1);
+    }
     const float g = vdb_lerp(vdb_lerp(vdb_lerp(d000, d001, w), vdb_lerp(d010, d011, w), v),
                              vdb_lerp(vdb_lerp(d100, d101, w), vdb_lerp(d110, d111, w), v), u);
     return M.multiplier * g;   // HeterogeneousMedium::getDensity (Src/medium.cpp:24-27)

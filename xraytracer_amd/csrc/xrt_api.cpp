@@ -404,6 +404,7 @@ int xrt_set_medium(xrt_ctx* c, const xrt_medium_desc* m) {
         D.scattering[q] = m->scattering[q];
     }
     D.voxel_size = m->voxel_size;
+    D.inv_voxel = 1.0 / (double)m->voxel_size;
     D.multiplier = m->density_multiplier;
     D.g = m->g;
     D.kind = XRT_MEDIUM_HETEROGENEOUS;
