@@ -226,6 +226,18 @@ def test_cornell_direct(renderer, sched):
     compare(img, ref)
 
 
+def test_deep_streams_wrap_the_ring(renderer, sched):
+    """~2,000-2,500 draws per pixel: every slot's stream position passes the ring's end
+    (1,248 words) more than once, so the vector RNG loads take their wrap-around branch
+    (a window that straddles the end) in every schedule, across many refills."""
+    s = scenes.cornell(16, 12)
+    for spp, kw in ((400, {}), (640, {"integrator": "direct"})):
+        img, ref, st = render_both(renderer, s, 16, 12, spp, schedule=sched, **kw)
+        compare(img, ref)
+        assert renderer.stats.draws == st["draws"]
+        assert st["draws"] / (16 * 12) > 2 * 1248 - 624   # the stream starts at word 624
+
+
 @pytest.mark.parametrize("wh", [(1, 1), (7, 3), (65, 33)])
 def test_edge_sizes(renderer, wh, sched):
     w, h = wh
