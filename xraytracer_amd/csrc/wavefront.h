@@ -143,6 +143,7 @@ struct KParams {
     const DObjBox* obj_box;   // per object, for the small-scene trace path (n_objs entries)
     const f4* bvh_node;       // large triangle scenes: BvhNode array (4 f4 each, bvh.h), else null
     const f4* bvh_tri;        // triangles in BVH leaf order, as `tri` but e2.w = original index
+    int bvh_stack;            // k_trace_bvh: LDS stack entries per thread (tree depth + 1 <= kBvhStack)
     const f4* snode;          // sphere scenes: threaded BVH (bvh.h SkipNode, 2 f4 each), else null
     const f4* ssph;           // spheres in BVH leaf order (center, radius)
     const int* sbk;           // per ssph entry: original sphere index | (occluder << 30)

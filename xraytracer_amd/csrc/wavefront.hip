@@ -309,7 +309,7 @@ __device__ bool bvh_trace(const KParams& P, uint32_t* stk, v3 o, v3 d, float tma
 template <int NL>
 __global__ __launch_bounds__(kBlock) void k_trace_bvh(KParams P, const uint32_t* __restrict__ list,
                                                        const uint32_t* __restrict__ count, uint32_t* zero_count) {
-    __shared__ uint32_t stack[kBvhStack * kBlock];
+    extern __shared__ uint32_t stack[];   // P.bvh_stack * kBlock entries: sized to the tree, so shallow trees fit more blocks per CU
     zero_parts(P, zero_count);
     const PartIter it = part_iter(P, count, kBlock);
     const int tid = threadIdx.x;
@@ -2153,10 +2153,12 @@ static hipError_t trace_nl(const KParams& P, const uint32_t* list, const uint32_
 hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
                         uint32_t blocks, hipStream_t st) {
     if (P.bvh_node && P.scene_kind == SCN_TRI) {
+        const size_t lds = (size_t)P.bvh_stack * kBlock * sizeof(uint32_t);
+        if (P.bvh_stack <= 0 || P.bvh_stack > kBvhStack) return hipErrorInvalidValue;
         if (P.n_lights <= 1)
-            hipLaunchKernelGGL((k_trace_bvh<1>), dim3(blocks), dim3(kBlock), 0, st, P, list, count, zero);
+            hipLaunchKernelGGL((k_trace_bvh<1>), dim3(blocks), dim3(kBlock), lds, st, P, list, count, zero);
         else
-            hipLaunchKernelGGL((k_trace_bvh<kMaxLights>), dim3(blocks), dim3(kBlock), 0, st, P, list, count, zero);
+            hipLaunchKernelGGL((k_trace_bvh<kMaxLights>), dim3(blocks), dim3(kBlock), lds, st, P, list, count, zero);
         return hipGetLastError();
     }
     if (P.small_tri) {
