@@ -144,6 +144,7 @@ struct KParams {
     const f4* bvh_node;       // large triangle scenes: BvhNode array (4 f4 each, bvh.h), else null
     const f4* bvh_tri;        // triangles in BVH leaf order, as `tri` but e2.w = original index
     int bvh_stack;            // k_trace_bvh: LDS stack entries per thread (tree depth + 1 <= kBvhStack)
+    int bvh_nodes;            // BvhNode count
     const f4* snode;          // sphere scenes: threaded BVH (bvh.h SkipNode, 2 f4 each), else null
     const f4* ssph;           // spheres in BVH leaf order (center, radius)
     const int* sbk;           // per ssph entry: original sphere index | (occluder << 30)

@@ -268,8 +268,8 @@ __device__ __forceinline__ float bvh_enter(const f4& mn, const f4& mx, v3 o, v3 
 // descend into the nearer child first (entry distance) and stack the farther one, so the
 // best t shrinks early and culls more of the tree; the result does not depend on the
 // order (lexicographic (t, index) minimum over every triangle whose box overlaps).
-template <bool ANY>
-__device__ bool bvh_trace(const KParams& P, uint32_t* stk, v3 o, v3 d, float tmax, float& bt, float& bu, float& bv,
+template <bool ANY, typename SE>
+__device__ bool bvh_trace(const KParams& P, SE* stk, v3 o, v3 d, float tmax, float& bt, float& bu, float& bv,
                           int& bk) {
     const v3 inv = rcp3(d);
     int sp = 0;
@@ -290,7 +290,7 @@ __device__ bool bvh_trace(const KParams& P, uint32_t* stk, v3 o, v3 d, float tma
         if (il && ir) {
             const bool lfirst = ANY || el <= er;
             next = __float_as_int(lfirst ? n0.w : n2.w);
-            stk[(sp++) * kBlock] = (uint32_t)__float_as_int(lfirst ? n2.w : n0.w);
+            stk[(sp++) * kBlock] = (SE)__float_as_int(lfirst ? n2.w : n0.w);
         } else if (il) {
             next = __float_as_int(n0.w);
         } else if (ir) {
@@ -306,14 +306,15 @@ __device__ bool bvh_trace(const KParams& P, uint32_t* stk, v3 o, v3 d, float tma
     return false;
 }
 
-template <int NL>
+template <int NL, typename SE>
 __global__ __launch_bounds__(kBlock) void k_trace_bvh(KParams P, const uint32_t* __restrict__ list,
                                                        const uint32_t* __restrict__ count, uint32_t* zero_count) {
-    extern __shared__ uint32_t stack[];   // P.bvh_stack * kBlock entries: sized to the tree, so shallow trees fit more blocks per CU
+    extern __shared__ uint32_t bvh_stack_lds[];   // P.bvh_stack * kBlock entries of SE: sized to the tree
+    SE* stack = reinterpret_cast<SE*>(bvh_stack_lds);
     zero_parts(P, zero_count);
     const PartIter it = part_iter(P, count, kBlock);
     const int tid = threadIdx.x;
-    uint32_t* stk = stack + tid;
+    SE* stk = stack + tid;
     for (uint32_t base = it.first; base < it.n; base += it.stride) {
         const uint32_t i = base + tid;
         if (i >= it.n) continue;
@@ -323,7 +324,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_bvh(KParams P, const uint32_t*
         if (st & ST_RAY) {
             float bt = kINF, bu = 0.0f, bv = 0.0f;
             int bk = -1;
-            (void)bvh_trace<false>(P, stk, xyz(P.ray_o[s]), xyz(P.ray_d[s]), kINF, bt, bu, bv, bk);
+            (void)bvh_trace<false, SE>(P, stk, xyz(P.ray_o[s]), xyz(P.ray_d[s]), kINF, bt, bu, bv, bk);
             P.hit[s] = make_float4(bt, bu, bv, __int_as_float(bk));
         }
         if (smask) {
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_bvh(KParams P, const uint32_t*
                 const f4 a = P.sh_o[(size_t)l * P.n_slots + s];
                 float bt = kINF, bu, bv;
                 int bk = -1;
-                if (bvh_trace<true>(P, stk, xyz(a), xyz(P.sh_d[(size_t)l * P.n_slots + s]), a.w, bt, bu, bv, bk))
+                if (bvh_trace<true, SE>(P, stk, xyz(a), xyz(P.sh_d[(size_t)l * P.n_slots + s]), a.w, bt, bu, bv, bk))
                     occ |= 1u << l;
             }
             P.occ[s] = occ;
@@ -2153,12 +2154,20 @@ static hipError_t trace_nl(const KParams& P, const uint32_t* list, const uint32_
 hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
                         uint32_t blocks, hipStream_t st) {
     if (P.bvh_node && P.scene_kind == SCN_TRI) {
-        const size_t lds = (size_t)P.bvh_stack * kBlock * sizeof(uint32_t);
         if (P.bvh_stack <= 0 || P.bvh_stack > kBvhStack) return hipErrorInvalidValue;
-        if (P.n_lights <= 1)
-            hipLaunchKernelGGL((k_trace_bvh<1>), dim3(blocks), dim3(kBlock), lds, st, P, list, count, zero);
+        // node indices below 2^16: 16-bit stack entries, half the LDS per thread
+        const bool small = P.bvh_nodes <= 0x10000;
+        const size_t lds = (size_t)P.bvh_stack * kBlock * (small ? sizeof(uint16_t) : sizeof(uint32_t));
+        if (small && P.n_lights <= 1)
+            hipLaunchKernelGGL((k_trace_bvh<1, uint16_t>), dim3(blocks), dim3(kBlock), lds, st, P, list, count, zero);
+        else if (small)
+            hipLaunchKernelGGL((k_trace_bvh<kMaxLights, uint16_t>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
+                               zero);
+        else if (P.n_lights <= 1)
+            hipLaunchKernelGGL((k_trace_bvh<1, uint32_t>), dim3(blocks), dim3(kBlock), lds, st, P, list, count, zero);
         else
-            hipLaunchKernelGGL((k_trace_bvh<kMaxLights>), dim3(blocks), dim3(kBlock), lds, st, P, list, count, zero);
+            hipLaunchKernelGGL((k_trace_bvh<kMaxLights, uint32_t>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
+                               zero);
         return hipGetLastError();
     }
     if (P.small_tri) {

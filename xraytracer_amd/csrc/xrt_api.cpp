@@ -297,7 +297,7 @@ int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
     // large triangle scenes: a BVH for the wavefront trace (C4's 51k-triangle sphere mesh).
     // Margin: 1e-4 of the scene diagonal + 1e-4, above the float error of a Moller-Trumbore
     // hit position, so box tests never drop a hit the linear scan accepts.
-    P.bvh_node = nullptr, P.bvh_tri = nullptr, P.bvh_stack = 0;
+    P.bvh_node = nullptr, P.bvh_tri = nullptr, P.bvh_stack = 0, P.bvh_nodes = 0;
     if (P.scene_kind == SCN_TRI && !P.small_tri && P.n_tris > 0 && !std::getenv("XRT_NO_BVH")) {
         const size_t nt = (size_t)P.n_tris;
         std::vector<float> mn(3 * nt), mx(3 * nt);
@@ -327,6 +327,7 @@ int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
             return rc;
         P.bvh_node = as<f4>(c->bvh_node), P.bvh_tri = as<f4>(c->bvh_tri);
         P.bvh_stack = B.depth + 1;
+        P.bvh_nodes = (int)B.nodes.size();
     }
     // sphere scenes (C3's 1001 spheres): a threaded BVH for the fused schedule's traces.
     // Sphere boxes: center +- radius, padded by 1e-4 of the scene diagonal + 1e-4 —
