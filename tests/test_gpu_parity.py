@@ -356,11 +356,12 @@ def test_normal_integrator_on_medium_box(renderer, sched):
     compare(img, ref)
 
 
-@pytest.mark.parametrize("nt,w,h,spp", [(24, 64, 36, 4), (80, 48, 30, 3)])
+@pytest.mark.parametrize("nt,w,h,spp", [(24, 64, 36, 4), (80, 48, 30, 3), (380, 12, 9, 2)])
 def test_c4_sphere_mesh_gi(renderer, nt, w, h, spp):
-    """Config C4 scene family (Cornell + tessellated sphere; 1,152 and 12,800 mesh triangles)
-    at reduced size: the wavefront schedule with BVH traces, bit-exact against the oracle's
-    linear scan, counters included."""
+    """Config C4 scene family (Cornell + tessellated sphere; 1,152, 12,800 and 288,800 mesh
+    triangles) at reduced size: the wavefront schedule with BVH traces, bit-exact against
+    the oracle's linear scan, counters included.  The largest tree has more than 65,536
+    nodes, so its traversal stack takes 32-bit entries (16-bit for the others)."""
     s = scenes.cornell_spheremesh(w, h, n_theta=nt, n_phi=nt)
     img, ref, st = render_both(renderer, s, w, h, spp)
     compare(img, ref)
