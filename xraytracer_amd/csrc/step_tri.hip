@@ -644,7 +644,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
 }
 
 // --------------------------------------------------------------- RNG refills ----
-// k_refill_merged: the merged schedule's ring refill.  Same twist as wave_twist (libstdc++
+// k_refill_merged: the ring refill of every schedule.  Same twist as wave_twist (libstdc++
 // _M_gen_rand: x[g+k] = x[g+k-227] ^ mix(x[g+k-624], x[g+k-623]), chunks k = m, 227+m,
 // 454+m held in registers), arranged for bandwidth: the old block is staged through LDS
 // (below), the next request's slot, stream position and old block are fetched while the
@@ -720,6 +720,9 @@ __device__ __forceinline__ void twist_block(uint32_t* ring, uint32_t g, int lane
     }
 }
 
+// CLEAR: also clear the slot's ST_RNGREQ (the wavefront / k_step schedules, whose kernels
+// test the flag; the merged kernel clears it itself when it next loads the slot).
+template <bool CLEAR>
 __global__ __launch_bounds__(kBlock) void k_refill_merged(KParams P, const uint32_t* __restrict__ req,
                                                           const uint32_t* __restrict__ count, uint32_t* zero_count) {
     __shared__ __attribute__((aligned(16))) uint32_t stage[kBlock / 64][2][kMT];
@@ -745,7 +748,10 @@ __global__ __launch_bounds__(kBlock) void k_refill_merged(KParams P, const uint3
             nx = load_block(P.ring + (size_t)sn * kRing, gn, lane);
         }
         twist_block(P.ring + (size_t)s * kRing, g, lane, stage[wv][buf]);
-        if (lane == 0) P.rng_g[s] = g + kMT;
+        if (lane == 0) {
+            P.rng_g[s] = g + kMT;
+            if (CLEAR) P.state[s] &= ~ST_RNGREQ;
+        }
         if (!more) break;
         store_block(nx, lane, stage[wv][buf ^ 1]);
         s = sn, g = gn, i = in;
@@ -756,7 +762,14 @@ hipError_t launch_refill_merged(const KParams& P, const uint32_t* count, uint32_
     // 16384 blocks (64 Ki waves) measured best on C2: 2048 7.7 ms, 4096 6.9, 8192 6.6, 16384 6.5
     // per frame (tools/refill_sweep.sh).
     const uint32_t per = std::max<uint32_t>(1u, std::min<uint32_t>((P.part_cap + 3) / 4, 16384u / P.n_part));
-    hipLaunchKernelGGL(k_refill_merged, dim3(P.n_part * per), dim3(kBlock), 0, st, P, P.req, count, zero_count);
+    hipLaunchKernelGGL(k_refill_merged<false>, dim3(P.n_part * per), dim3(kBlock), 0, st, P, P.req, count,
+                       zero_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_refill(const KParams& P, const uint32_t* count, uint32_t* zero_count, hipStream_t st) {
+    const uint32_t per = std::max<uint32_t>(1u, std::min<uint32_t>((P.part_cap + 3) / 4, 16384u / P.n_part));
+    hipLaunchKernelGGL(k_refill_merged<true>, dim3(P.n_part * per), dim3(kBlock), 0, st, P, P.req, count, zero_count);
     return hipGetLastError();
 }
 

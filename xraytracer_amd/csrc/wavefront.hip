@@ -19,24 +19,6 @@
 
 namespace xrt {
 
-// k_refill: one wave per requested slot twists the next 624 words of its stream into the
-// consumed half of its ring (wave_twist), all requests in parallel across the chip.
-// Also clears the request counter the next epoch appends to.
-__global__ __launch_bounds__(kBlock) void k_refill(KParams P, const uint32_t* __restrict__ req,
-                                                    const uint32_t* __restrict__ count, uint32_t* zero_count) {
-    zero_parts(P, zero_count);
-    const PartIter it = part_iter(P, count, kBlock / 64);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (uint32_t i = it.first + wv; i < it.n; i += it.stride) {
-        const uint32_t s = req[it.p * P.part_cap + i];
-        const uint32_t g = P.rng_g[s];
-        wave_twist(P.ring + (size_t)s * kRing, g, lane);
-        if (lane == 0) {
-            P.rng_g[s] = g + kMT;
-            P.state[s] &= ~ST_RNGREQ;
-        }
-    }
-}
 
 // ==================================================================== k_seed ====
 // mt19937::seed(j + width*i) for every slot (Src/renderer.cpp:35-36).  The recurrence is
@@ -2134,12 +2116,6 @@ hipError_t launch_seed(const KParams& P, uint32_t* list, uint32_t* count, uint32
     return hipGetLastError();
 }
 
-hipError_t launch_refill(const KParams& P, const uint32_t* count, uint32_t* zero_count, hipStream_t st) {
-    const uint32_t per = std::max<uint32_t>(1u, std::min<uint32_t>((P.part_cap + 3) / 4, 2048u / P.n_part));
-    const uint32_t blocks = P.n_part * per;
-    hipLaunchKernelGGL(k_refill, dim3(blocks), dim3(kBlock), 0, st, P, P.req, count, zero_count);
-    return hipGetLastError();
-}
 
 template <int SCN>
 static hipError_t trace_nl(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
