@@ -1,5 +1,5 @@
 #!/bin/bash
-# tools/pmc_c5.sh — PMC passes over C4's wavefront trace/shade kernels (64 spp: per-launch
+# tools/pmc_c5.sh — PMC passes over C5's fused k_step (VolumePathTracing, 64 spp: per-launch
 # counters are what matter), one counter group per rocprofv3 run.
 set -uo pipefail
 O=gpurun_out/pmc_c5; mkdir -p $O; export TMPDIR=/tmp
