@@ -140,6 +140,35 @@ BvhBuild build_bvh(const float* prim_min, const float* prim_max, uint32_t n, uin
     }
     B.out.order.resize(n);
     for (uint32_t i = 0; i < n; ++i) B.out.order[i] = B.refs[i].idx;
+    // Renumber so the first kBvhTopNodes nodes in breadth-first order come first (the
+    // trace kernel keeps them in LDS); the rest keep their depth-first order.  Traversal
+    // results do not depend on node numbering.
+    std::vector<BvhNode>& nodes = B.out.nodes;
+    const size_t nn = nodes.size();
+    std::vector<int32_t> remap(nn, -1);
+    std::vector<uint32_t> order;
+    order.reserve(nn);
+    if (nn) order.push_back(0), remap[0] = 0;
+    for (size_t head = 0; head < order.size() && order.size() < std::min<size_t>(nn, kBvhTopNodes); ++head) {
+        const BvhNode& nd = nodes[order[head]];
+        for (int c = 0; c < 2; ++c) {
+            const int32_t idx = c ? nd.right : nd.left, cnt = c ? nd.rcount : nd.lcount;
+            if (cnt == 0 && order.size() < std::min<size_t>(nn, kBvhTopNodes)) {
+                remap[(size_t)idx] = (int32_t)order.size();
+                order.push_back((uint32_t)idx);
+            }
+        }
+    }
+    for (size_t i = 0; i < nn; ++i)
+        if (remap[i] < 0) remap[i] = (int32_t)order.size(), order.push_back((uint32_t)i);
+    std::vector<BvhNode> out(nn);
+    for (size_t i = 0; i < nn; ++i) {
+        BvhNode nd = nodes[order[i]];
+        if (nd.lcount == 0) nd.left = remap[(size_t)nd.left];
+        if (nd.rcount == 0) nd.right = remap[(size_t)nd.right];
+        out[i] = nd;
+    }
+    nodes.swap(out);
     return std::move(B.out);
 }
 

@@ -15,6 +15,7 @@
 // (Src/renderer.cpp:29-81).
 #include <hip/hip_runtime.h>
 
+#include "bvh.h"
 #include "path_common.h"
 
 namespace xrt {
@@ -250,15 +251,22 @@ __device__ __forceinline__ float bvh_enter(const f4& mn, const f4& mx, v3 o, v3 
 // descend into the nearer child first (entry distance) and stack the farther one, so the
 // best t shrinks early and culls more of the tree; the result does not depend on the
 // order (lexicographic (t, index) minimum over every triangle whose box overlaps).
+// top: the first ntop nodes (the breadth-first top of the tree, host/bvh.cpp) in LDS.
 template <bool ANY, typename SE>
-__device__ bool bvh_trace(const KParams& P, SE* stk, v3 o, v3 d, float tmax, float& bt, float& bu, float& bv,
-                          int& bk) {
+__device__ bool bvh_trace(const KParams& P, const f4* top, int ntop, SE* stk, v3 o, v3 d, float tmax, float& bt,
+                          float& bu, float& bv, int& bk) {
     const v3 inv = rcp3(d);
     int sp = 0;
     int node = 0;
     while (true) {
-        const f4* N = P.bvh_node + 4 * (size_t)node;
-        const f4 n0 = N[0], n1 = N[1], n2 = N[2], n3 = N[3];
+        f4 n0, n1, n2, n3;
+        if (node < ntop) {
+            const f4* N = top + 4 * node;
+            n0 = N[0], n1 = N[1], n2 = N[2], n3 = N[3];
+        } else {
+            const f4* N = P.bvh_node + 4 * (size_t)node;
+            n0 = N[0], n1 = N[1], n2 = N[2], n3 = N[3];
+        }
         const float lim = ANY ? tmax : bt;
         const int lcount = __float_as_int(n1.w), rcount = __float_as_int(n3.w);
         const float el = lcount >= 0 ? bvh_enter(n0, n1, o, inv, lim) : __builtin_inff();
@@ -291,11 +299,17 @@ __device__ bool bvh_trace(const KParams& P, SE* stk, v3 o, v3 d, float tmax, flo
 template <int NL, typename SE>
 __global__ __launch_bounds__(kBlock) void k_trace_bvh(KParams P, const uint32_t* __restrict__ list,
                                                        const uint32_t* __restrict__ count, uint32_t* zero_count) {
-    extern __shared__ uint32_t bvh_stack_lds[];   // P.bvh_stack * kBlock entries of SE: sized to the tree
-    SE* stack = reinterpret_cast<SE*>(bvh_stack_lds);
+    // LDS: the top min(bvh_nodes, kBvhTopNodes) nodes, then P.bvh_stack * kBlock stack
+    // entries of SE (sized to the tree)
+    extern __shared__ uint32_t bvh_stack_lds[];
+    const int tid = threadIdx.x;
+    const int ntop = P.bvh_nodes < (int)kBvhTopNodes ? P.bvh_nodes : (int)kBvhTopNodes;
+    f4* top = reinterpret_cast<f4*>(bvh_stack_lds);
+    for (int q = tid; q < 4 * ntop; q += kBlock) top[q] = P.bvh_node[q];
+    SE* stack = reinterpret_cast<SE*>(bvh_stack_lds + 16 * ntop);
+    __syncthreads();
     zero_parts(P, zero_count);
     const PartIter it = part_iter(P, count, kBlock);
-    const int tid = threadIdx.x;
     SE* stk = stack + tid;
     for (uint32_t base = it.first; base < it.n; base += it.stride) {
         const uint32_t i = base + tid;
@@ -306,7 +320,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_bvh(KParams P, const uint32_t*
         if (st & ST_RAY) {
             float bt = kINF, bu = 0.0f, bv = 0.0f;
             int bk = -1;
-            (void)bvh_trace<false, SE>(P, stk, xyz(P.ray_o[s]), xyz(P.ray_d[s]), kINF, bt, bu, bv, bk);
+            (void)bvh_trace<false, SE>(P, top, ntop, stk, xyz(P.ray_o[s]), xyz(P.ray_d[s]), kINF, bt, bu, bv, bk);
             P.hit[s] = make_float4(bt, bu, bv, __int_as_float(bk));
         }
         if (smask) {
@@ -317,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_bvh(KParams P, const uint32_t*
                 const f4 a = P.sh_o[(size_t)l * P.n_slots + s];
                 float bt = kINF, bu, bv;
                 int bk = -1;
-                if (bvh_trace<true, SE>(P, stk, xyz(a), xyz(P.sh_d[(size_t)l * P.n_slots + s]), a.w, bt, bu, bv, bk))
+                if (bvh_trace<true, SE>(P, top, ntop, stk, xyz(a), xyz(P.sh_d[(size_t)l * P.n_slots + s]), a.w, bt, bu, bv, bk))
                     occ |= 1u << l;
             }
             P.occ[s] = occ;
@@ -2133,7 +2147,8 @@ hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* 
         if (P.bvh_stack <= 0 || P.bvh_stack > kBvhStack) return hipErrorInvalidValue;
         // node indices below 2^16: 16-bit stack entries, half the LDS per thread
         const bool small = P.bvh_nodes <= 0x10000;
-        const size_t lds = (size_t)P.bvh_stack * kBlock * (small ? sizeof(uint16_t) : sizeof(uint32_t));
+        const size_t ntop = std::min<size_t>((size_t)P.bvh_nodes, kBvhTopNodes);
+        const size_t lds = ntop * 4 * sizeof(f4) + (size_t)P.bvh_stack * kBlock * (small ? sizeof(uint16_t) : sizeof(uint32_t));
         if (small && P.n_lights <= 1)
             hipLaunchKernelGGL((k_trace_bvh<1, uint16_t>), dim3(blocks), dim3(kBlock), lds, st, P, list, count, zero);
         else if (small)
