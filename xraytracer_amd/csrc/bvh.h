@@ -19,7 +19,7 @@ namespace xrt {
 // A child with count > 0 is a leaf of `count` primitives starting at `index` of the
 // reordered primitive array; count == 0 is an interior node at `index`; count == -1 is an
 // empty slot (a one-leaf tree's right child).
-constexpr uint32_t kBvhTopNodes = 128;   // leading nodes (breadth-first) the BVH trace keeps in LDS
+constexpr uint32_t kBvhTopNodes = 64;   // leading nodes (breadth-first) the BVH trace keeps in LDS
 
 struct BvhNode {
     float lmin[3];
