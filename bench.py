@@ -20,6 +20,11 @@ sys.path.insert(0, ROOT)
 METRIC = "Msamples/s (whole node) + wall-clock at 800×600×1024spp, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3        # vector FP32 spec
+# VALU issue peak: 256 CUs x 4 SIMD-32 units, a wave64 vector instruction issues over 2
+# cycles (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles"), 2.4 GHz max
+# clock -> 1,024 * 2.4e9 / 2 = 1,228.8 G wave-instructions/s (= the FP32 vector peak / 128)
+SIMDS, CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 2
+VALU_PEAK_GINST = SIMDS * CLOCK_HZ / VALU_CYCLES / 1e9
 
 # Roofline model: algorithmic bytes per sample of the
 # path, B_s = 68 + 264·Q + 12·D, with Q = extension segments per sample and D = RNG draws
@@ -42,12 +47,23 @@ def env_int(k, d):
         return d
 
 
+def cpu_quota():
+    """CPUs the cgroup lets this process use (cpu.max quota / period), or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(p)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(cfg_name, cfg, spp):
-    """The oracle (CPU restatement, bit-exact with the GPU path) on this host's cores."""
+    """The oracle (CPU restatement, bit-exact with the GPU path) on every core this process
+    may run on (os.sched_getaffinity), one OpenMP thread per core."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     from xraytracer_amd import scenes
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = max(1, len(os.sched_getaffinity(0)))
+    quota = cpu_quota()
     s = scenes.build(cfg_name)
     w, h = cfg["width"], cfg["height"]
     t0 = time.perf_counter()
@@ -55,7 +71,8 @@ def cpu_baseline(cfg_name, cfg, spp):
     dt = time.perf_counter() - t0
     return {"value": round(w * h * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"{cfg_name} scene {w}x{h} at {spp} spp (cost is linear in spp), oracle/oracle.c "
-                      f"with OpenMP over rows, {dt:.2f} s wall"}
+                      f"with OpenMP over rows on all {threads} affinity cores"
+                      + (f" (cgroup CPU quota {quota:g})" if quota else "") + f", {dt:.2f} s wall"}
 
 
 def main():
@@ -70,6 +87,7 @@ def main():
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--schedule", default="auto", choices=("auto", "wavefront"))
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     args = ap.parse_args()
 
     import numpy as np
@@ -101,8 +119,11 @@ def main():
     timing = not args.no_timing
 
     def step(timed):
+        # the render waits for the work queued on torch's stream (the previous step's reduce)
+        # before it overwrites fb (xrt_render_device_after)
         st = r.render_device(scene, W, H, fb.data_ptr(), shard_index=rank, shard_count=world,
-                             timing=timing and timed, schedule=args.schedule)
+                             timing=timing and timed, schedule=args.schedule,
+                             after_stream=torch.cuda.current_stream(dev).cuda_stream)
         distributed.reduce_framebuffer(fb, dist)
         return st
 
@@ -168,11 +189,47 @@ def main():
                         traffic = tj.get("hbm_bytes_per_launch")
                 except (OSError, ValueError):
                     traffic = None
-            roof = {"bound": "hbm", "kernel": "k_" + kname, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            # measured limiter, from the PMC passes of the same kernel and workload
+            # (tools/profile.sh -> tools/prof_summary.py -> profiles/pmc_latest.json):
+            #   VALU issue: SQ_INSTS_VALU per launch / avg launch time vs VALU_PEAK_GINST
+            #   HBM:        (FETCH_SIZE x2 + WRITE_SIZE) per launch / avg launch time vs 8 TB/s
+            pmc = None
+            if os.path.exists(args.pmc):
+                try:
+                    pj = json.load(open(args.pmc))
+                    if pj.get("config") == args.config and pj.get("kernel") == "k_" + kname:
+                        pmc = pj
+                except (OSError, ValueError):
+                    pmc = None
+            model = {"what": "SURVEY.md 8d algorithmic bytes, B_s = 68 + 264*Q + 12*D per sample",
+                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "bytes_per_sample": round(b_s, 2),
+                     "algorithmic_bytes_per_launch": round(per_launch, 1)}
+            hbm = None
+            if traffic:
+                hbm = {"achieved": round(traffic / avg_s / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 5), "bytes_per_launch": traffic}
+            valu = None
+            if pmc and pmc.get("SQ_INSTS_VALU_per_launch"):
+                vi = pmc["SQ_INSTS_VALU_per_launch"]
+                valu = {"achieved": round(vi / avg_s / 1e9, 2), "peak": round(VALU_PEAK_GINST, 1),
+                        "unit": "Gwave-inst/s", "frac": round(vi / avg_s / 1e9 / VALU_PEAK_GINST, 5),
+                        "valu_insts_per_launch": vi,
+                        "valu_insts_per_sample": round(vi * kl[dom] / max(1.0, samples), 2),
+                        "lane_utilisation": pmc.get("lane_utilisation"),
+                        "valu_active_per_wave_cycle": pmc.get("valu_active_per_wave_cycle"),
+                        "wait_per_wave_cycle": pmc.get("wait_per_wave_cycle")}
+            if valu and (not hbm or valu["frac"] >= hbm["frac"]):
+                head, bound = valu, "valu"
+            elif hbm:
+                head, bound = hbm, "hbm"
+            else:   # no counters for this build: the model figure, labelled as such
+                head, bound = model, "hbm (model; unmeasured)"
+            roof = {"bound": bound, "kernel": "k_" + kname, "achieved": head["achieved"], "peak": head["peak"],
+                    "unit": head["unit"], "frac": head["frac"], "traffic": traffic,
                     "avg_launch_us": round(avg_s * 1e6, 3), "launches": int(kl[dom]),
-                    "algorithmic_bytes_per_launch": round(per_launch, 1),
-                    "bytes_per_sample": round(b_s, 2), "model": "SURVEY.md 8d: B_s = 68 + 264*Q + 12*D"}
+                    "valu_issue": valu, "hbm_measured": hbm, "model": model,
+                    "pmc_source": (pmc or {}).get("source")}
             # secondary: the reference's brute-force triangle tests (every object, every
             # triangle; shadow rays skip area-light objects) x FLOP_PER_TRI_TEST — only for
             # the small triangle scenes whose traces are (culled) linear scans

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 7
+#define XRT_ABI_VERSION 8
 
 /* ---- status codes ---------------------------------------------------------------- */
 enum {
@@ -125,8 +125,15 @@ enum {
     XRT_FLAG_TIMING = 1u,      /* time every kernel with HIP events (xrt_stats.kernel_ms)     */
     XRT_FLAG_WAVEFRONT = 2u,   /* force the multi-pass schedule (k_shade + k_trace) even when
                                   the scene fits the fused LDS-resident schedule (k_step)     */
-    XRT_FLAG_NO_MERGED = 4u    /* triangle scenes: per-segment cooperative traces (k_step_tri)
+    XRT_FLAG_NO_MERGED = 4u,   /* triangle scenes: per-segment cooperative traces (k_step_tri)
                                   instead of the merged shadow + extension traces             */
+    XRT_FLAG_NO_GROUP = 8u,    /* merged schedule with 16/32 slots per wave: spread the traces
+                                  over idle lanes (pair passes) instead of 4/2-lane groups    */
+    XRT_FLAG_ACCUMULATE = 16u  /* Renderer::render's in-place contract (Src/renderer.cpp:75,98):
+                                  each owned pixel starts from the value already in the output
+                                  buffer (Image::addPixel adds to it in sample order), then
+                                  /= spp; pixels of other shards are left untouched.  Without
+                                  the flag the buffer is overwritten (zeros outside the shard). */
 };
 
 typedef struct {
@@ -137,6 +144,10 @@ typedef struct {
     uint32_t shard_index;    /* this rank owns image rows y with y % shard_count == idx */
     uint32_t shard_count;    /* 1 = whole image                                         */
     uint32_t flags;          /* XRT_FLAG_*                                              */
+    /* launch geometry of the merged schedule; 0 = chosen by the library from the shard's
+     * slot count.  Results never depend on these (tests render every layout). */
+    uint32_t slots_per_wave;    /* 0, 16, 32 or 64 path slots per 64-lane wave           */
+    uint32_t visits_per_launch; /* 0 or 1..128 path segments per slot per step launch    */
 } xrt_render_params;
 
 enum {
@@ -162,6 +173,11 @@ typedef struct {
     uint64_t path_slots;         /* slots in flight (pixels of this shard)                 */
     uint64_t schedule;           /* XRT_SCHED_* the render ran                             */
     uint64_t stalled;            /* paths stopped by the VPT no-progress guard             */
+    /* launch geometry the render ran with (merged schedule; 0 otherwise) */
+    uint32_t slots_per_wave;     /* path slots per wave                                    */
+    uint32_t group_lanes;        /* lanes sharing one slot's traces (1 = pair passes)      */
+    uint32_t partitions;         /* live-list partitions                                   */
+    uint32_t visits_per_launch;  /* path segments per slot per step launch                 */
 } xrt_stats;
 
 /* ---- context ----------------------------------------------------------------------- */
@@ -183,8 +199,16 @@ int  xrt_set_medium(xrt_ctx* ctx, const xrt_medium_desc* medium);
  * j + width*i).  Pixels outside this shard are written as 0.  Blocks until done. */
 int  xrt_render(xrt_ctx* ctx, const xrt_render_params* p, float* rgb_out, xrt_stats* st);
 /* Same, writing into a DEVICE pointer on this context's GPU (e.g. a torch tensor), so a
- * multi-GPU caller can reduce framebuffers over RCCL without a host round trip. */
+ * multi-GPU caller can reduce framebuffers over RCCL without a host round trip.
+ * Ordering: the render starts only after all work previously queued on the device has
+ * finished (a device-wide wait), so it never overwrites d_rgb_out while a collective or
+ * copy issued by the caller still reads it.  Returns after the image is complete. */
 int  xrt_render_device(xrt_ctx* ctx, const xrt_render_params* p, float* d_rgb_out, xrt_stats* st);
+/* As xrt_render_device, but waits only for the work queued so far on `hip_stream` (a
+ * hipStream_t of this context's GPU, e.g. torch.cuda.current_stream().cuda_stream; NULL =
+ * the legacy default stream) before touching d_rgb_out. */
+int  xrt_render_device_after(xrt_ctx* ctx, const xrt_render_params* p, float* d_rgb_out, void* hip_stream,
+                             xrt_stats* st);
 
 /* Output stage: Image::gammaCorrection(gamma) then writePPM's 8-bit quantisation
  * (Src/image.h:80-114) on the device, for n_pixels float3 pixels: d_rgb is a DEVICE

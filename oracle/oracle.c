@@ -929,11 +929,10 @@ static v3 integrate(const scene_ctx* C, const xrt_render_params* p, v3 ro, v3 rd
  * records.  Returns the accumulated (not yet divided) pixel sum. */
 static v3 do_render_pixel(const scene_ctx* C, const orc_camera* cam, const xrt_render_params* p,
                           uint32_t i, uint32_t j, path_counters* pc, uint64_t* draws, uint64_t* rejected,
-                          float* rec_rad, uint32_t* rec_draws, uint32_t* rec_segs) {
+                          float* rec_rad, uint32_t* rec_draws, uint32_t* rec_segs, v3 acc) {
     const uint32_t width = p->width, height = p->height;
     orc_mt rng;
     orc_mt_seed(&rng, j + width * i);
-    v3 acc = mk(0, 0, 0);
     for (uint32_t k = 0; k < p->spp; ++k) {
         uint64_t d0 = rng.draws, s0 = pc->segments;
         const float u = ((float)(int)j + orc_draw(&rng)) / (float)width;
@@ -967,7 +966,10 @@ int orc_render(const xrt_scene_desc* S, const orc_camera* cam, const xrt_medium_
     if (check_params(S, p, M)) return XRT_ERR_INVALID;
     scene_ctx C;
     setup_ctx(&C, S, M);
-    memset(rgb_out, 0, sizeof(float) * 3 * (size_t)p->width * p->height);
+    /* XRT_FLAG_ACCUMULATE: the reference's Image is filled in place — addPixel adds every
+     * sample to what the pixel already holds (Src/renderer.cpp:75, image.h:46-50) */
+    const int accumulate = (p->flags & XRT_FLAG_ACCUMULATE) != 0;
+    if (!accumulate) memset(rgb_out, 0, sizeof(float) * 3 * (size_t)p->width * p->height);
     uint64_t segs = 0, shadows = 0, draws = 0, rejected = 0, tests = 0, stalled = 0, ub = 0, samples = 0;
     const int64_t rows = p->height;
 #ifdef _OPENMP
@@ -979,10 +981,12 @@ int orc_render(const xrt_scene_desc* S, const orc_camera* cam, const xrt_medium_
         if (i % p->shard_count != p->shard_index) continue;
         path_counters pc = {0, 0, 0, 0, 0};
         for (uint32_t j = 0; j < p->width; ++j) {
-            v3 acc = do_render_pixel(&C, cam, p, i, j, &pc, &draws, &rejected, NULL, NULL, NULL);
+            float* px = rgb_out + ((size_t)j + (size_t)p->width * i) * 3;
+            const v3 acc0 = accumulate ? mk(px[0], px[1], px[2]) : mk(0, 0, 0);
+            v3 acc = do_render_pixel(&C, cam, p, i, j, &pc, &draws, &rejected, NULL, NULL, NULL, acc0);
             /* Image::operator/= (Src/image.h:69-78) with Vec3f(n_samples) */
             const float n = (float)p->spp;
-            st3(rgb_out + ((size_t)j + (size_t)p->width * i) * 3, vdivv(acc, mk(n, n, n)));
+            st3(px, vdivv(acc, mk(n, n, n)));
             samples += p->spp;
         }
         segs += pc.segments;
@@ -1008,7 +1012,7 @@ int orc_trace_pixels(const xrt_scene_desc* S, const orc_camera* cam, const xrt_m
         path_counters pc = {0, 0, 0, 0, 0};
         uint64_t dr = 0, rj = 0;
         (void)do_render_pixel(&C, cam, p, pix_i[q], pix_j[q], &pc, &dr, &rj, rad + (size_t)q * p->spp * 3,
-                              draws + (size_t)q * p->spp, segs + (size_t)q * p->spp);
+                              draws + (size_t)q * p->spp, segs + (size_t)q * p->spp, mk(0, 0, 0));
     }
     return XRT_OK;
 }

@@ -100,10 +100,15 @@ def params(scene, width, height, spp, shard_index=0, shard_count=1, integrator=N
     return p
 
 
-def render(scene, width, height, spp, nthreads=0, **kw):
-    """NormalRenderer::render restated on the CPU: returns ((H,W,3) float32, stats dict)."""
+def render(scene, width, height, spp, nthreads=0, initial=None, **kw):
+    """NormalRenderer::render restated on the CPU: returns ((H,W,3) float32, stats dict).
+    initial: the Image's prior contents — samples are added to them in place before the
+    divide, as the reference's render does (XRT_FLAG_ACCUMULATE); None = a zero image."""
     p = params(scene, width, height, spp, **kw)
     img = np.zeros((height, width, 3), np.float32)
+    if initial is not None:
+        img[...] = initial
+        p.flags |= abi.XRT_FLAG_ACCUMULATE
     st = OrcStats()
     med = scene.medium.desc() if scene.medium is not None else None
     rc = lib().orc_render(C.byref(scene.desc), C.byref(camera(scene.camera)),

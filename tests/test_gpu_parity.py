@@ -47,11 +47,14 @@ EXPECT_TRI = {"auto": abi.XRT_SCHED_STEP_MERGED, "step_tri": abi.XRT_SCHED_STEP_
               "wavefront": abi.XRT_SCHED_WAVEFRONT}
 
 
+GPU_ONLY = ("slots_per_wave", "visits_per_launch", "group")   # launch geometry, not semantics
+
+
 def render_both(r, scene, w, h, spp, schedule="auto", **kw):
     r.spp = spp
     r._uploaded = None
     img = r.render(scene, w, h, schedule=schedule, **kw)
-    ref, st = pyoracle.render(scene, w, h, spp, **kw)
+    ref, st = pyoracle.render(scene, w, h, spp, **{k: v for k, v in kw.items() if k not in GPU_ONLY})
     steps = r.stats.launches[abi.XRT_K_STEP]
     if schedule == "wavefront":
         assert steps == 0
@@ -255,34 +258,31 @@ def test_spp_one_and_depth_zero(renderer, sched):
 
 
 @pytest.mark.parametrize("visits", [1, 2, 3, 7])
-def test_merged_segments_per_launch(renderer, visits, monkeypatch):
+def test_merged_segments_per_launch(renderer, visits):
     """The merged-trace kernel drains its shadow rays at every launch boundary and resumes
     paths across launches: any number of segments per launch gives the same image and
     counters (GI and Direct; one and two lights)."""
-    monkeypatch.setenv("XRT_STEP_VISITS", str(visits))
     s = scenes.cornell(24, 18)
     for kw in ({}, {"integrator": "direct"}, {"max_depth": 5}):
-        img, ref, st = render_both(renderer, s, 24, 18, 6, **kw)
+        img, ref, st = render_both(renderer, s, 24, 18, 6, visits_per_launch=visits, **kw)
         compare(img, ref)
         g = renderer.stats
-        assert g.schedule == abi.XRT_SCHED_STEP_MERGED
+        assert g.schedule == abi.XRT_SCHED_STEP_MERGED and g.visits_per_launch == visits
         assert (g.segments, g.shadow_rays, g.draws) == (st["segments"], st["shadow_rays"], st["draws"])
 
 
 @pytest.mark.parametrize("spw,group", [(16, True), (32, True), (64, True), (16, False), (32, False)])
-def test_merged_slots_per_wave(renderer, spw, group, monkeypatch):
+def test_merged_slots_per_wave(renderer, spw, group):
     """The merged kernel's layouts for small pixel shards — 16 or 32 slots per wave, their
     traces shared by 4 or 2 lanes per slot (group trace) or spread over idle lanes
     (cooperative passes) — render the same image and counters as full waves."""
-    monkeypatch.setenv("XRT_MERGED_SPW", str(spw))
-    if not group:
-        monkeypatch.setenv("XRT_NO_GROUP", "1")
     s = scenes.cornell(40, 30)
     for kw in ({}, {"integrator": "direct"}):
-        img, ref, st = render_both(renderer, s, 40, 30, 5, **kw)
+        img, ref, st = render_both(renderer, s, 40, 30, 5, slots_per_wave=spw, group=group, **kw)
         compare(img, ref)
         g = renderer.stats
         assert g.schedule == abi.XRT_SCHED_STEP_MERGED
+        assert (g.slots_per_wave, g.group_lanes) == (spw, 64 // spw if group and spw < 64 else 1)
         assert (g.segments, g.shadow_rays, g.draws) == (st["segments"], st["shadow_rays"], st["draws"])
 
 

@@ -17,8 +17,8 @@ print(re.search(r"(k_\w+)", top["Name"]).group(1))
 PY
 )
 python3 "$R/tools/prof_summary.py" "$R/gpurun_out/$TAG" "$KPAT" --traffic "$CFG" "$R/profiles/traffic_latest.json" \
-    > "$R/gpurun_out/$TAG/summary.txt"
+    --pmc "$CFG" "$R/profiles/pmc_latest.json" --csv "$R/gpurun_out/$TAG/pmc_dispatch.csv" > "$R/gpurun_out/$TAG/summary.txt"
 cp "$R/gpurun_out/$TAG/kt/kt_kernel_stats.csv" "$R/gpurun_out/$TAG/kt_kernel_stats.csv"
-mkdir -p "$R/gpurun_out/profiles_new" && cp "$R/profiles/traffic_latest.json" "$R/gpurun_out/profiles_new/"
+mkdir -p "$R/gpurun_out/profiles_new" && cp "$R/profiles/traffic_latest.json" "$R/profiles/pmc_latest.json" "$R/gpurun_out/profiles_new/"
 timeout -k 10 600 python3 "$R/bench.py" --config "$CFG" > "$R/gpurun_out/$TAG/bench.json"
 cat "$R/gpurun_out/$TAG/bench.json"

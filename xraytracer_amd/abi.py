@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(HERE, "libxrt_hip.so")
 if os.environ.get("XRT_LIB"):   # experiment builds (csrc/Makefile `variant`), same ABI
     LIB_PATH = os.path.join(HERE, os.environ["XRT_LIB"])
 
-XRT_ABI_VERSION = 7   # include/xrt.h XRT_ABI_VERSION
+XRT_ABI_VERSION = 8   # include/xrt.h XRT_ABI_VERSION
 XRT_OK = 0
 XRT_OBJ_MESH, XRT_OBJ_SPHERE, XRT_OBJ_BOX = 0, 1, 2
 XRT_LIGHT_QUAD, XRT_LIGHT_TRIANGLE, XRT_LIGHT_SPHERE = 0, 1, 2
@@ -24,7 +24,7 @@ XRT_MAT_NONE, XRT_MAT_LAMBERT = 0, 1
 XRT_INTEGRATOR_GI, XRT_INTEGRATOR_DIRECT, XRT_INTEGRATOR_VPT = 0, 1, 2
 XRT_INTEGRATOR_INDIRECT, XRT_INTEGRATOR_NORMAL, XRT_INTEGRATOR_VPT_NEE = 3, 4, 5
 XRT_MEDIUM_HETEROGENEOUS, XRT_MEDIUM_HOMOGENEOUS_MIS, XRT_MEDIUM_HOMOGENEOUS_ACHROMATIC, XRT_MEDIUM_HOMOGENEOUS_NOMIS = 0, 1, 2, 3
-XRT_FLAG_TIMING, XRT_FLAG_WAVEFRONT, XRT_FLAG_NO_MERGED = 1, 2, 4
+XRT_FLAG_TIMING, XRT_FLAG_WAVEFRONT, XRT_FLAG_NO_MERGED, XRT_FLAG_NO_GROUP, XRT_FLAG_ACCUMULATE = 1, 2, 4, 8, 16
 XRT_SCHED_WAVEFRONT, XRT_SCHED_STEP, XRT_SCHED_STEP_TRI, XRT_SCHED_STEP_MERGED = 0, 1, 2, 3
 SCHEDULE_NAMES = ("wavefront", "step", "step_tri", "step_merged")
 XRT_K_SEED, XRT_K_TRACE, XRT_K_SHADE, XRT_K_FINISH, XRT_K_STEP, XRT_K_REFILL, XRT_K_COUNT = 0, 1, 2, 3, 4, 5, 6
@@ -69,7 +69,8 @@ class XrtMediumDesc(C.Structure):
 class XrtRenderParams(C.Structure):
     _fields_ = [("integrator", C.c_int32), ("max_depth", C.c_uint32), ("width", C.c_uint32),
                 ("height", C.c_uint32), ("spp", C.c_uint32), ("shard_index", C.c_uint32),
-                ("shard_count", C.c_uint32), ("flags", C.c_uint32)]
+                ("shard_count", C.c_uint32), ("flags", C.c_uint32), ("slots_per_wave", C.c_uint32),
+                ("visits_per_launch", C.c_uint32)]
 
 
 class XrtStats(C.Structure):
@@ -77,7 +78,8 @@ class XrtStats(C.Structure):
                 ("launches", C.c_uint64 * XRT_K_COUNT), ("samples", C.c_uint64),
                 ("segments", C.c_uint64), ("shadow_rays", C.c_uint64), ("draws", C.c_uint64),
                 ("rejected", C.c_uint64), ("iterations", C.c_uint64), ("path_slots", C.c_uint64),
-                ("schedule", C.c_uint64), ("stalled", C.c_uint64)]
+                ("schedule", C.c_uint64), ("stalled", C.c_uint64), ("slots_per_wave", C.c_uint32),
+                ("group_lanes", C.c_uint32), ("partitions", C.c_uint32), ("visits_per_launch", C.c_uint32)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "launches")}
@@ -97,6 +99,8 @@ SIGNATURES = {
     "xrt_set_medium": (C.c_int, [C.c_void_p, C.POINTER(XrtMediumDesc)]),
     "xrt_render": (C.c_int, [C.c_void_p, C.POINTER(XrtRenderParams), f32p, C.POINTER(XrtStats)]),
     "xrt_render_device": (C.c_int, [C.c_void_p, C.POINTER(XrtRenderParams), C.c_void_p, C.POINTER(XrtStats)]),
+    "xrt_render_device_after": (C.c_int, [C.c_void_p, C.POINTER(XrtRenderParams), C.c_void_p, C.c_void_p,
+                                          C.POINTER(XrtStats)]),
     "xrt_hscene_create": (C.c_void_p, []),
     "xrt_hscene_destroy": (None, [C.c_void_p]),
     "xrt_hscene_last_error": (C.c_char_p, [C.c_void_p]),

@@ -91,5 +91,6 @@ void HipRenderer::render(const Scene& scene, Sampler::SamplerType, Image& image)
     p.spp = n_samples;
     p.shard_index = 0;
     p.shard_count = 1;
+    p.flags = XRT_FLAG_ACCUMULATE;   // samples are added to the Image in place (Src/renderer.cpp:75, 98)
     if ((rc = xrt_render(m_ctx, &p, image.data(), &m_stats)) != XRT_OK) return fail(rc, "xrt_render");
 }

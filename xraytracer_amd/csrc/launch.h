@@ -9,6 +9,13 @@
 #include "wavefront.h"
 
 namespace xrt {
+// Experiment switches (tools/*.sh) are read from the environment only in builds made with
+// -DXRT_EXPERIMENTS (csrc/Makefile `variant`); the shipped library never reads them.
+#ifdef XRT_EXPERIMENTS
+inline const char* exp_env(const char* name) { return std::getenv(name); }
+#else
+inline const char* exp_env(const char*) { return nullptr; }
+#endif
 hipError_t launch_seed(const KParams& P, uint32_t* list, uint32_t* count, uint32_t* count_other,
                        uint32_t* req_count, hipStream_t st);
 // twist the rings of the slots on P.req (count at *count); clears *zero_count
@@ -32,6 +39,7 @@ hipError_t launch_step(const KParams& P, const KParams* dP, const uint32_t* list
 bool use_step_merged(const KParams& P);
 uint32_t step_merged_draws(const KParams& P);
 uint32_t step_merged_spw(const KParams& P, uint64_t live);   // slots per wave for `live` live slots
+uint32_t step_merged_group(const KParams& P, uint32_t spw);  // lanes per slot in group traces (1 = none)
 size_t step_merged_lds_bytes(const KParams& P);
 void build_step_objs(const DObjBox* boxes, int n, StepObjs& SO);
 hipError_t launch_step_merged(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,

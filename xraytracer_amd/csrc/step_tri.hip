@@ -777,7 +777,7 @@ hipError_t launch_refill(const KParams& P, const uint32_t* count, uint32_t* zero
 bool use_step_merged(const KParams& P) {
     return P.scene_kind == SCN_TRI && P.small_tri && P.n_objs <= kMergedMaxObjs && P.n_lights <= kMaxLights &&
            (P.integrator == XRT_INTEGRATOR_DIRECT || (P.integrator == XRT_INTEGRATOR_GI && P.max_depth > 0)) &&
-           !std::getenv("XRT_NO_MERGED") && step_merged_lds_bytes(P) <= kStepLds;
+           !exp_env("XRT_NO_MERGED") && step_merged_lds_bytes(P) <= kStepLds;
 }
 
 uint32_t step_merged_draws(const KParams& P) { return 6u + 2u * (uint32_t)P.n_lights; }
@@ -828,12 +828,9 @@ static void launch_merged_i(const KParams& P, const KParams* dP, const StepObjs&
 }
 
 // slots per wave for a shard of `live` slots
-// (XRT_MERGED_SPW overrides, for experiments; results do not depend on it)
+// (xrt_render_params.slots_per_wave overrides it; results do not depend on it)
 uint32_t step_merged_spw(const KParams& P, uint64_t live) {
-    if (const char* e = std::getenv("XRT_MERGED_SPW")) {
-        const int v = std::atoi(e);
-        if (v == 16 || v == 32 || v == 64) return (uint32_t)v;
-    }
+    if (P.spw_req == 16 || P.spw_req == 32 || P.spw_req == 64) return P.spw_req;
     // measured on C2 (tools/shard_sim.py): full waves down to ~160k live
     // slots, 32 slots per wave down to ~90k, then 16 (4 lanes per slot)
     if (live >= kMergedLive64) return 64;
@@ -841,12 +838,18 @@ uint32_t step_merged_spw(const KParams& P, uint64_t live) {
     return 16;
 }
 
+// lanes that share one slot's traces at `spw` slots per wave (1 = pair passes over the wave)
+uint32_t step_merged_group(const KParams& P, uint32_t spw) {
+    const bool group = P.n_tris <= 64 && !(P.rflags & XRT_FLAG_NO_GROUP);   // group trace: 64-bit triangle masks
+    return spw < 64 && group ? 64u / spw : 1u;
+}
+
 template <int INTEG>
 static void launch_merged_spw(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                               const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
                               uint32_t* req_count, uint32_t visits, uint64_t live, size_t lds, hipStream_t st) {
-    const bool group = P.n_tris <= 64 && !std::getenv("XRT_NO_GROUP");   // group trace: 64-bit triangle masks
-    const bool lane64 = group && std::getenv("XRT_LANE_TRACE");   // experiment: per-lane traces, full waves
+    const bool group = P.n_tris <= 64 && !(P.rflags & XRT_FLAG_NO_GROUP);   // group trace: 64-bit triangle masks
+    const bool lane64 = group && exp_env("XRT_LANE_TRACE");   // experiment: per-lane traces, full waves
 #define XRT_MERGED_CASE(SPWV, GV, LV) \
     launch_merged_i<INTEG, SPWV, GV, LV>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, lds, st)
     switch (step_merged_spw(P, live)) {

@@ -159,6 +159,8 @@ struct KParams {
     uint32_t max_depth, width, height, spp, shard_index, shard_count, n_slots;
     uint32_t n_part, part_cap;   // live-list partitions: n_part (<= kMaxParts) of part_cap slots
     uint32_t rng_keep;           // fused schedule refill threshold (words ahead)
+    uint32_t spw_req;            // merged schedule: requested slots per wave (0 = by live count)
+    uint32_t rflags;             // xrt_render_params.flags
     // ---- slot state (SoA)
     f4 *ray_o, *ray_d, *thr, *rad, *thr_prev;
     f4 *hit;     // t, u, v, code(bits)        code: -1 miss, (kind << 28) | prim

@@ -2245,7 +2245,7 @@ static hipError_t step_i(const KParams& P, const uint32_t* list, const uint32_t*
 
 bool use_step_tri(const KParams& P) {
     return P.scene_kind == SCN_TRI && P.small_tri && P.n_objs <= kCoopMaxObjs &&
-           (P.integrator == XRT_INTEGRATOR_GI || P.integrator == XRT_INTEGRATOR_DIRECT) && !std::getenv("XRT_NO_COOP") &&
+           (P.integrator == XRT_INTEGRATOR_GI || P.integrator == XRT_INTEGRATOR_DIRECT) && !exp_env("XRT_NO_COOP") &&
            ((step_layout(P).total + 15u) & ~15u) + (kBlock / 64) * sizeof(CoopWave) <= kStepLds;
 }
 

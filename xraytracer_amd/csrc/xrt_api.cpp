@@ -51,6 +51,8 @@ struct xrt_ctx {
     size_t cap_fb = 0;
     uint32_t* h_poll = nullptr;  // pinned
     std::vector<hipEvent_t> events;
+    hipEvent_t poll_ev[8] = {};  // live-count polls of render_impl (created once)
+    hipEvent_t wait_ev = nullptr;   // xrt_render_device_after: the caller stream's position
 };
 
 namespace {
@@ -103,12 +105,6 @@ T* as(DevBuf& b) {
 
 uint32_t shard_rows(uint32_t h, uint32_t idx, uint32_t n) { return idx < h ? (h - idx + n - 1) / n : 0; }
 
-uint32_t env_u32(const char* name, uint32_t dflt, uint32_t lo, uint32_t hi) {
-    const char* v = std::getenv(name);
-    if (!v || !*v) return dflt;
-    const long x = std::strtol(v, nullptr, 10);
-    return (uint32_t)std::min<long>(hi, std::max<long>(lo, x));
-}
 
 }  // namespace
 
@@ -125,10 +121,16 @@ int xrt_create(int device, xrt_ctx** out) {
     xrt_ctx* c = new xrt_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&c->h_poll, 8 * kMaxParts * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
-        delete c;
+        hipHostMalloc((void**)&c->h_poll, 8 * kMaxParts * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming) != hipSuccess) {
+        xrt_destroy(c);
         return XRT_ERR_HIP;
     }
+    for (hipEvent_t& e : c->poll_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            xrt_destroy(c);
+            return XRT_ERR_HIP;
+        }
     *out = c;
     return XRT_OK;
 }
@@ -144,6 +146,9 @@ void xrt_destroy(xrt_ctx* c) {
                      &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch, &c->kparams};
     for (DevBuf* b : all) free_buf(*b);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->poll_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->wait_ev) (void)hipEventDestroy(c->wait_ev);
     if (c->h_poll) (void)hipHostFree(c->h_poll);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -155,6 +160,9 @@ const char* xrt_last_error(const xrt_ctx* c) { return c ? c->err.c_str() : "no c
 // so the linear scan order equals Scene::intersect's order (Src/scene.cpp:190-200).
 int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
     if (!c || !s) return XRT_ERR_INVALID;
+    // a failed upload (OOM, bad range) must not leave the previous scene's freed buffers
+    // behind a valid-looking context: renders are refused until an upload completes
+    c->has_scene = false;
     HIPCHK(c, hipSetDevice(c->device));
     if (s->n_lights > (uint32_t)kMaxLights)
         return set_err(c, XRT_ERR_UNSUPPORTED, "more than " + std::to_string(kMaxLights) + " area lights");
@@ -298,7 +306,7 @@ int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
     // Margin: 1e-4 of the scene diagonal + 1e-4, above the float error of a Moller-Trumbore
     // hit position, so box tests never drop a hit the linear scan accepts.
     P.bvh_node = nullptr, P.bvh_tri = nullptr, P.bvh_stack = 0, P.bvh_nodes = 0;
-    if (P.scene_kind == SCN_TRI && !P.small_tri && P.n_tris > 0 && !std::getenv("XRT_NO_BVH")) {
+    if (P.scene_kind == SCN_TRI && !P.small_tri && P.n_tris > 0 && !exp_env("XRT_NO_BVH")) {
         const size_t nt = (size_t)P.n_tris;
         std::vector<float> mn(3 * nt), mx(3 * nt);
         float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
@@ -334,7 +342,7 @@ int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
     // far above the float error of Sphere::intersect's hit point (and of its
     // near-tangent discriminant), so a box test never drops a hit the linear scan accepts.
     P.snode = nullptr, P.ssph = nullptr, P.sbk = nullptr, P.n_snode = 0;
-    if (P.scene_kind == SCN_SPHERE && P.n_sph >= kSphBvhMin && !std::getenv("XRT_NO_BVH")) {
+    if (P.scene_kind == SCN_SPHERE && P.n_sph >= kSphBvhMin && !exp_env("XRT_NO_BVH")) {
         const size_t ns = (size_t)P.n_sph;
         std::vector<float> mn(3 * ns), mx(3 * ns);
         float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
@@ -421,7 +429,10 @@ int xrt_set_medium(xrt_ctx* c, const xrt_medium_desc* m) {
     return XRT_OK;
 }
 
-static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, float* h_out, xrt_stats* st) {
+// wait: 0 = none (host output: the library owns the framebuffer), 1 = the whole device
+// (xrt_render_device), 2 = the caller's stream `wait_stream` (xrt_render_device_after)
+static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, float* h_out, xrt_stats* st,
+                       int wait = 0, hipStream_t wait_stream = nullptr) {
     const auto t_start = std::chrono::steady_clock::now();
     if (!c || !p) return XRT_ERR_INVALID;
     if (!c->has_scene || !c->has_camera) return set_err(c, XRT_ERR_STATE, "upload a scene and set a camera first");
@@ -434,11 +445,37 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
         return set_err(c, XRT_ERR_STATE, "VolumePathTracing needs xrt_set_medium first");
     if (p->integrator == XRT_INTEGRATOR_VPT_NEE && c->base.n_lights == 0)
         return set_err(c, XRT_ERR_STATE, "VolumePathTracingNEE needs an area light");
+    if (p->slots_per_wave != 0 && p->slots_per_wave != 16 && p->slots_per_wave != 32 && p->slots_per_wave != 64)
+        return set_err(c, XRT_ERR_INVALID, "slots_per_wave must be 0, 16, 32 or 64");
+    if (p->visits_per_launch > 128) return set_err(c, XRT_ERR_INVALID, "visits_per_launch must be 0..128");
     HIPCHK(c, hipSetDevice(c->device));
+    if (wait == 1) {
+        HIPCHK(c, hipDeviceSynchronize());
+    } else if (wait == 2) {
+        HIPCHK(c, hipEventRecord(c->wait_ev, wait_stream));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->wait_ev, 0));
+    }
     const uint32_t rows = shard_rows(p->height, p->shard_index, p->shard_count);
     const size_t n = (size_t)rows * p->width;
     const size_t npix = (size_t)p->width * p->height;
     int rc;
+    if (n == 0) {
+        // a shard that owns no rows (shard_index >= height): an all-zero framebuffer
+        float* fb0 = d_out;
+        if (!fb0) {
+            if ((rc = ensure(c, c->fb, npix * 3 * sizeof(float)))) return rc;
+            fb0 = as<float>(c->fb);
+        }
+        if (p->flags & XRT_FLAG_ACCUMULATE) return XRT_OK;   // nothing owned, nothing touched
+        HIPCHK(c, hipMemsetAsync(fb0, 0, npix * 3 * sizeof(float), c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (h_out) HIPCHK(c, hipMemcpy(h_out, fb0, npix * 3 * sizeof(float), hipMemcpyDeviceToHost));
+        if (st) {
+            std::memset(st, 0, sizeof(*st));
+            st->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+        }
+        return XRT_OK;
+    }
     if (n > c->cap_slots) {
         const size_t L = kMaxLights;
         if ((rc = ensure(c, c->ray_o, n * 16)) || (rc = ensure(c, c->ray_d, n * 16)) || (rc = ensure(c, c->thr, n * 16)) ||
@@ -465,6 +502,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     P.integrator = p->integrator;
     P.max_depth = p->max_depth, P.width = p->width, P.height = p->height, P.spp = p->spp;
     P.shard_index = p->shard_index, P.shard_count = p->shard_count, P.n_slots = (uint32_t)n;
+    P.spw_req = p->slots_per_wave, P.rflags = p->flags;
     // live-list partitions: up to kMaxParts (a multiple of the 8 XCDs), >= 2048 slots each
     {
         uint32_t np = (uint32_t)std::min<size_t>(kMaxParts, std::max<size_t>(1, n / 2048));
@@ -518,7 +556,10 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
         return err;
     };
 
-    HIPCHK(c, hipMemsetAsync(fb, 0, npix * 3 * sizeof(float), c->stream));
+    if (!(p->flags & XRT_FLAG_ACCUMULATE))
+        HIPCHK(c, hipMemsetAsync(fb, 0, npix * 3 * sizeof(float), c->stream));
+    else if (h_out)   // the caller's Image is the accumulator (Src/renderer.cpp:75)
+        HIPCHK(c, hipMemcpyAsync(fb, h_out, npix * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(P.stats, 0, 512, c->stream));
     HIPCHK(c, launch(XRT_K_SEED, [&] { return launch_seed(P, lists[0], counts_at(0), counts_at(1), req_counts, c->stream); }));
     // refill epochs: shading launches of epoch e append to req_counts[e & 1]; k_refill(e)
@@ -547,12 +588,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     constexpr uint64_t kPoll = 16, kAhead = 64;
     struct Poll { uint64_t it; hipEvent_t ev; int slot; };
     std::vector<Poll> polls;
-    std::vector<hipEvent_t> poll_ev;
-    for (int q = 0; q < 8; ++q) {
-        hipEvent_t e;
-        HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        poll_ev.push_back(e);
-    }
+    hipEvent_t* poll_ev = c->poll_ev;
     uint64_t it = 0;
     int poll_slot = 0;
     bool done = false;
@@ -564,20 +600,20 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     // to counts[(i+1)%3] and clears counts[(i+2)%3] for round i+1.
     const bool fused = !(p->flags & XRT_FLAG_WAVEFRONT) && step_lds_bytes(P) != 0;
     const bool merged = fused && !(p->flags & XRT_FLAG_NO_MERGED) && use_step_merged(P);
-    // tuning knobs (defaults kStepVisits / kStepRefill; XRT_STEP_VISITS / XRT_STEP_REFILL
-    // override them for experiments — results do not depend on them)
+    // segments per slot per step launch: kMergedVisits / kStepVisits unless the caller
+    // sets visits_per_launch (results do not depend on it)
     const uint32_t merged_visits =
         merged ? std::min<uint32_t>(kMergedVisits, (kMT - step_merged_draws(P)) / step_merged_draws(P)) : 0;
-    const uint32_t step_visits = env_u32("XRT_STEP_VISITS", merged ? merged_visits : kStepVisits, 1, 128);
+    const uint32_t step_visits = p->visits_per_launch ? p->visits_per_launch : merged ? merged_visits : kStepVisits;
     // the merged kernel relies on one refill launch after every step launch (it clears
-    // ST_RNGREQ itself), so XRT_STEP_REFILL does not apply to it
-    const uint32_t step_refill = merged ? 1u : env_u32("XRT_STEP_REFILL", kStepRefill, 1, 8);
+    // ST_RNGREQ itself)
+    const uint32_t step_refill = merged ? 1u : kStepRefill;
     merged_refill = merged;
     // a slot queues a refill when fewer words are left than the next `refill` launches can
     // draw: the merged kernel draws at most step_merged_draws per segment and checks it
     P.rng_keep = merged ? step_refill * step_visits * step_merged_draws(P) + step_merged_draws(P)
                         : step_refill * step_visits * kVisitDraws + kRngVisit;
-    if (P.rng_keep > kMT) return set_err(c, XRT_ERR_INVALID, "XRT_STEP_VISITS * XRT_STEP_REFILL too large");
+    if (P.rng_keep > kMT) return set_err(c, XRT_ERR_INVALID, "visits_per_launch too large for the RNG ring");
     // device copy of the (now final) parameters for kernels that read them from memory
     if ((rc = ensure(c, c->kparams, sizeof(KParams)))) return rc;
     HIPCHK(c, hipMemcpyAsync(c->kparams.p, &P, sizeof(KParams), hipMemcpyHostToDevice, c->stream));
@@ -649,7 +685,6 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     S.iterations = it;
     HIPCHK(c, launch(XRT_K_FINISH, [&] { return launch_finish(P, c->stream); }));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    for (hipEvent_t e : poll_ev) (void)hipEventDestroy(e);
     if (!done) {
         // the iteration cap was reached without observing an empty list: verify
         uint32_t left[kMaxParts] = {0};
@@ -674,8 +709,14 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     S.schedule = !fused ? XRT_SCHED_WAVEFRONT
                  : merged ? XRT_SCHED_STEP_MERGED
                  : use_step_tri(P) ? XRT_SCHED_STEP_TRI : XRT_SCHED_STEP;
+    S.partitions = P.n_part;
+    if (fused) S.visits_per_launch = step_visits;
+    if (merged) {
+        S.slots_per_wave = step_merged_spw(P, live_hint);
+        S.group_lanes = step_merged_group(P, S.slots_per_wave);
+    }
     if (timing) {
-        const bool trace = std::getenv("XRT_TRACE_LAUNCHES") != nullptr;   // experiments: per-launch times
+        const bool trace = exp_env("XRT_TRACE_LAUNCHES") != nullptr;   // experiments: per-launch times
         for (size_t q = 0; q < ev_use.size(); ++q) {
             const auto& u = ev_use[q];
             float ms = 0.0f;
@@ -707,7 +748,13 @@ int xrt_render(xrt_ctx* c, const xrt_render_params* p, float* rgb_out, xrt_stats
 
 int xrt_render_device(xrt_ctx* c, const xrt_render_params* p, float* d_rgb_out, xrt_stats* st) {
     if (!d_rgb_out) return set_err(c, XRT_ERR_INVALID, "null output");
-    return render_impl(c, p, d_rgb_out, nullptr, st);
+    return render_impl(c, p, d_rgb_out, nullptr, st, 1);
+}
+
+int xrt_render_device_after(xrt_ctx* c, const xrt_render_params* p, float* d_rgb_out, void* hip_stream,
+                            xrt_stats* st) {
+    if (!d_rgb_out) return set_err(c, XRT_ERR_INVALID, "null output");
+    return render_impl(c, p, d_rgb_out, nullptr, st, 2, (hipStream_t)hip_stream);
 }
 
 // ---------------------------------------------------------------- self-tests ----

@@ -51,11 +51,15 @@ class HipRenderer:
         self._uploaded = scene
 
     def params(self, scene, width, height, shard_index=0, shard_count=1, timing=False, integrator=None,
-               max_depth=None, schedule="auto"):
+               max_depth=None, schedule="auto", slots_per_wave=0, visits_per_launch=0, group=True,
+               accumulate=False):
         """schedule: "auto" (fused k_step when the scene fits in LDS — for small triangle
         scenes with merged shadow + extension traces — else the multi-pass wavefront),
         "wavefront" (always k_shade + k_trace) or "step_tri" (fused, one cooperative trace
-        per ray kind instead of the merged traces)."""
+        per ray kind instead of the merged traces).  slots_per_wave / visits_per_launch /
+        group fix the merged schedule's launch geometry (0 / True = the library's choice);
+        results never depend on them.  accumulate: add the samples to the output buffer's
+        current contents before the divide (XRT_FLAG_ACCUMULATE, Renderer::render's contract)."""
         if schedule not in ("auto", "wavefront", "step_tri"):
             raise ValueError(f"unknown schedule {schedule!r}")
         p = abi.XrtRenderParams()
@@ -64,15 +68,20 @@ class HipRenderer:
         p.width, p.height, p.spp = width, height, self.spp
         p.shard_index, p.shard_count = shard_index, shard_count
         p.flags = ((abi.XRT_FLAG_TIMING if timing else 0) | (abi.XRT_FLAG_WAVEFRONT if schedule == "wavefront" else 0) |
-                   (abi.XRT_FLAG_NO_MERGED if schedule == "step_tri" else 0))
+                   (abi.XRT_FLAG_NO_MERGED if schedule == "step_tri" else 0) | (0 if group else abi.XRT_FLAG_NO_GROUP) |
+                   (abi.XRT_FLAG_ACCUMULATE if accumulate else 0))
+        p.slots_per_wave, p.visits_per_launch = slots_per_wave, visits_per_launch
         return p
 
-    def render(self, scene: SceneBundle, width: int, height: int, **kw) -> np.ndarray:
-        """Render into a host (H, W, 3) float32 image."""
+    def render(self, scene: SceneBundle, width: int, height: int, initial=None, **kw) -> np.ndarray:
+        """Render into a host (H, W, 3) float32 image.  initial: the Image's prior contents,
+        accumulated into in place as Renderer::render does (XRT_FLAG_ACCUMULATE)."""
         if self._uploaded is not scene:
             self.upload(scene)
-        p = self.params(scene, width, height, **kw)
+        p = self.params(scene, width, height, accumulate=initial is not None, **kw)
         img = np.zeros((height, width, 3), np.float32)
+        if initial is not None:
+            img[...] = initial
         st = abi.XrtStats()
         self._check(self._lib.xrt_render(self.ctx, C.byref(p), abi.fptr(img), C.byref(st)), "xrt_render")
         self.stats = st
@@ -95,13 +104,20 @@ class HipRenderer:
             f.write(f"P3\n{w} {h}\n255\n")
             f.write("".join(f"{r} {g} {b}\n" for r, g, b in rgb8.reshape(-1, 3).tolist()))
 
-    def render_device(self, scene: SceneBundle, width: int, height: int, out_ptr: int, **kw):
-        """Render into a device buffer (e.g. torch tensor .data_ptr()) of H*W*3 float32."""
+    def render_device(self, scene: SceneBundle, width: int, height: int, out_ptr: int, after_stream=None, **kw):
+        """Render into a device buffer (e.g. torch tensor .data_ptr()) of H*W*3 float32.
+        after_stream: a HIP stream handle (torch.cuda.current_stream().cuda_stream) whose
+        queued work must finish before the buffer is overwritten; None = wait for the whole
+        device.  Returns when the image is complete."""
         if self._uploaded is not scene:
             self.upload(scene)
         p = self.params(scene, width, height, **kw)
         st = abi.XrtStats()
-        self._check(self._lib.xrt_render_device(self.ctx, C.byref(p), C.c_void_p(out_ptr), C.byref(st)),
-                    "xrt_render_device")
+        if after_stream is None:
+            rc = self._lib.xrt_render_device(self.ctx, C.byref(p), C.c_void_p(out_ptr), C.byref(st))
+        else:
+            rc = self._lib.xrt_render_device_after(self.ctx, C.byref(p), C.c_void_p(out_ptr),
+                                                   C.c_void_p(after_stream or None), C.byref(st))
+        self._check(rc, "xrt_render_device")
         self.stats = st
         return st
