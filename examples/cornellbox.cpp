@@ -2,14 +2,16 @@
 // the same scene, camera and integrator construction, with HipRenderer in place of
 // NormalRenderer/ParallelRenderer.
 //
-//   cornellbox [width height spp integrator(gi|direct) out.raw]
+//   cornellbox [width height spp integrator(gi|direct) out.raw devices]
 // writes the linear framebuffer (height*width*3 float32) to out.raw (default
-// cornellbox.ppm, gamma 1.2, like the reference example).
+// cornellbox.ppm, gamma 1.2, like the reference example).  devices: a comma-separated GPU
+// list ("0,1,2,3") renders with the multi-GPU HipRenderer (ParallelRenderer over the node).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include <xrt/camera.h>
 #include <xrt/image.h>
@@ -51,7 +53,15 @@ int main(int argc, char** argv) {
     if (kind == "direct") integrator = std::make_unique<DirectIntegrator>();
     else integrator = std::make_unique<GIIntegrator>(max_depth);
 
-    auto renderer = std::make_unique<HipRenderer>(n_samples, camera.get(), integrator.get());
+    std::vector<int> devices;
+    for (const char* p = argc > 6 ? argv[6] : ""; *p;) {
+        devices.push_back((int)std::strtol(p, const_cast<char**>(&p), 10));
+        if (*p == ',') ++p;
+        else break;
+    }
+    auto renderer = devices.size() > 1
+                        ? std::make_unique<HipRenderer>(n_samples, camera.get(), integrator.get(), devices)
+                        : std::make_unique<HipRenderer>(n_samples, camera.get(), integrator.get());
     renderer->render(scene, Sampler::SamplerType::Uniform, image);
     if (renderer->lastStatus() != 0) {
         std::fprintf(stderr, "render failed: %s\n", renderer->lastError().c_str());

@@ -17,8 +17,11 @@
  *
  * Conventions: plain C types only; the caller owns all host memory and the library
  * copies what it needs; status 0 = XRT_OK, negative = error (xrt_last_error gives
- * text); no C++ exception crosses this boundary.  One context = one GPU = one host
- * thread; multi-GPU runs one process (and one context) per GPU.
+ * text); no C++ exception crosses this boundary.  A context is used by one host thread.
+ * Multi-GPU, two ways: one process per GPU with one context each, rendering row shards
+ * (shard_index / shard_count) and reducing the framebuffers over RCCL (the bench); or one
+ * process with one context over several GPUs (xrt_create_multi), which shards and
+ * assembles the frame itself (ParallelRenderer over the node, Src/renderer.cpp:83-99).
  */
 #ifndef XRT_H
 #define XRT_H
@@ -186,6 +189,14 @@ typedef struct xrt_ctx xrt_ctx;
 int  xrt_abi_version(void);
 /* device = HIP device ordinal (one process per GPU: LOCAL_RANK) */
 int  xrt_create(int device, xrt_ctx** out);
+/* One context over n_devices GPUs (HIP ordinals; a device may be listed twice, e.g. to
+ * exercise the multi-GPU path on one GPU).  Every call fans out to all of them; a render
+ * gives device i the interleaved rows y % (n * shard_count) == shard_index + shard_count * i
+ * (one host thread and HIP stream per device, concurrently) and assembles the frame on
+ * devices[0] with one strided peer copy per device — bit-identical to a one-GPU render.
+ * xrt_render_device* take a device pointer on devices[0]. */
+int  xrt_create_multi(const int* devices, int n_devices, xrt_ctx** out);
+int  xrt_device_count(const xrt_ctx* ctx);   /* GPUs a context renders on */
 void xrt_destroy(xrt_ctx* ctx);
 const char* xrt_last_error(const xrt_ctx* ctx);   /* ctx may be NULL (create failure) */
 

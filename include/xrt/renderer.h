@@ -5,6 +5,7 @@
 #pragma once
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "camera.h"
 #include "image.h"
@@ -27,6 +28,9 @@ struct xrt_ctx;
 class HipRenderer : public Renderer {
 public:
     HipRenderer(uint32_t spp, Camera* cam, Integrator* inte, int device = 0);
+    // ParallelRenderer over several GPUs (Src/renderer.cpp:83-99): the image's rows are
+    // interleaved over `devices` and assembled on devices[0] (xrt_create_multi)
+    HipRenderer(uint32_t spp, Camera* cam, Integrator* inte, std::vector<int> devices);
     ~HipRenderer() override;
     // Errors are reported like the reference reports them (logged; the image is left as
     // rendered so far); lastStatus()/lastError() expose them to callers that care.
@@ -38,6 +42,7 @@ public:
 private:
     const uint32_t n_samples;
     int m_device;
+    std::vector<int> m_devices;   // empty: one GPU (m_device)
     mutable xrt_ctx* m_ctx = nullptr;
     mutable int m_status = 0;
     mutable std::string m_error;

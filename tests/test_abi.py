@@ -36,3 +36,5 @@ def test_null_arguments_are_rejected_without_a_gpu():
     assert lib.xrt_render(None, None, None, None) != 0
     assert lib.xrt_upload_scene(None, None) == -1
     assert lib.xrt_last_error(None)
+    assert lib.xrt_create_multi(None, 0, None) == -1
+    assert lib.xrt_device_count(None) == 0

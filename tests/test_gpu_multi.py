@@ -1,0 +1,80 @@
+"""Multi-GPU inside the library (xrt_create_multi; the C++ HipRenderer(spp, cam, integ,
+devices) of ParallelRenderer, Src/renderer.cpp:83-99): row shards rendered concurrently
+per device and assembled on the first device by strided peer copies.
+
+The GPU box has one MI355X, so the device list names GPU 0 several times: every device
+context, host thread, stream and the row gather run exactly as on a node, only on one
+card.  The frame must be bit-identical to the one-GPU render and to the oracle.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import pyoracle
+from xraytracer_amd import abi, scenes
+from xraytracer_amd.renderer import HipRenderer
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def single():
+    r = HipRenderer(4, device=0)
+    yield r
+    r.close()
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_multi_matches_single_and_oracle(single, n):
+    s = scenes.cornell(96, 71)
+    m = HipRenderer(4, devices=[0] * n)
+    assert abi.lib().xrt_device_count(m.ctx) == n
+    img = m.render(s, 96, 71, timing=True)
+    ref, st = pyoracle.render(s, 96, 71, 4)
+    assert np.array_equal(img, ref)
+    g = m.stats
+    assert (g.samples, g.segments, g.shadow_rays, g.draws) == (96 * 71 * 4, st["segments"], st["shadow_rays"],
+                                                               st["draws"])
+    single.spp = 4
+    assert np.array_equal(single.render(s, 96, 71), img)
+    # the caller's own row shard, split again over the devices
+    part = m.render(s, 96, 71, shard_index=1, shard_count=2)
+    assert np.array_equal(part[1::2], ref[1::2]) and np.all(part[0::2] == 0)
+    m.close()
+
+
+def test_multi_device_output_accumulate_and_media():
+    import torch
+
+    m = HipRenderer(3, devices=[0, 0])
+    s = scenes.cornell(64, 48)
+    init = np.random.default_rng(1).uniform(0, 2, (48, 64, 3)).astype(np.float32)
+    ref, _ = pyoracle.render(s, 64, 48, 3, initial=init)
+    assert np.array_equal(m.render(s, 64, 48, initial=init), ref)
+    fb = torch.from_numpy(init).to("cuda:0")
+    m.render_device(s, 64, 48, fb.data_ptr(), accumulate=True)
+    assert np.array_equal(fb.cpu().numpy(), ref)
+    fb.fill_(9.0)
+    m.render_device(s, 64, 48, fb.data_ptr(), after_stream=torch.cuda.current_stream().cuda_stream)
+    plain, _ = pyoracle.render(s, 64, 48, 3)
+    assert np.array_equal(fb.cpu().numpy(), plain)
+    # the medium is uploaded to every device (VolumePathTracing, fused k_step<VPT>)
+    v = scenes.smoke(40, 30, n=32)
+    ref, st = pyoracle.render(v, 40, 30, 3)
+    assert np.array_equal(m.render(v, 40, 30), ref)
+    assert m.stats.draws == st["draws"]
+    m.close()
+
+
+def test_cpp_multi_gpu_renderer(tmp_path):
+    """examples/cornellbox.cpp with a device list: HipRenderer(spp, cam, integ, {0, 0})."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "examples", "bin", "cornellbox")
+    out = tmp_path / "fb.raw"
+    env = dict(os.environ, XRT_DATA_DIR=os.path.join(root, "xraytracer_amd", "data") + "/")
+    subprocess.check_call([exe, "64", "48", "4", "gi", str(out), "0,0"], env=env)
+    img = np.fromfile(out, dtype=np.float32).reshape(48, 64, 3)
+    ref, _ = pyoracle.render(scenes.cornell(64, 48), 64, 48, 4)
+    assert np.array_equal(img, ref)

@@ -22,6 +22,8 @@ def main():
     cfg_name = sys.argv[1] if len(sys.argv) > 1 else "C2"
     timing = "--timing" in sys.argv
     only = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--only=")]
+    spw = ([int(a.split("=")[1]) for a in sys.argv if a.startswith("--spw=")] or [0])[0]
+    group = "--no-group" not in sys.argv
     cfg = scenes.CONFIGS[cfg_name]
     W, H, SPP = cfg["width"], cfg["height"], cfg["spp"]
     scene = scenes.build(cfg_name)
@@ -35,7 +37,8 @@ def main():
         for s in (sorted({0, n - 1}) if not only else [0]):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            st = r.render_device(scene, W, H, fb.data_ptr(), shard_index=s, shard_count=n, timing=timing)
+            st = r.render_device(scene, W, H, fb.data_ptr(), shard_index=s, shard_count=n, timing=timing,
+                                 slots_per_wave=spw, group=group)
             torch.cuda.synchronize()
             times.append(time.perf_counter() - t0)
         slow = max(times)

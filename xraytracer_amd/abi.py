@@ -92,6 +92,8 @@ class XrtStats(C.Structure):
 SIGNATURES = {
     "xrt_abi_version": (C.c_int, []),
     "xrt_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "xrt_create_multi": (C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_void_p)]),
+    "xrt_device_count": (C.c_int, [C.c_void_p]),
     "xrt_destroy": (None, [C.c_void_p]),
     "xrt_last_error": (C.c_char_p, [C.c_void_p]),
     "xrt_upload_scene": (C.c_int, [C.c_void_p, C.POINTER(XrtSceneDesc)]),
@@ -134,6 +136,15 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() "
                               "(the HIP path has no CPU fallback)")
+        # PyTorch-ROCm wheels bundle their own HIP runtime.  Once /opt/rocm's runtime (which
+        # libxrt_hip links) is loaded, torch's own fails to initialise later in the same
+        # process ("No HIP GPUs are available"; measured on the MI355X box), while the other
+        # order works.  Load torch first when it is installed, so callers can render into
+        # torch tensors (xrt_render_device) in any import order.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         l = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(l, name)

@@ -10,6 +10,9 @@
 HipRenderer::HipRenderer(uint32_t spp, Camera* cam, Integrator* inte, int device)
     : Renderer(cam, inte), n_samples(spp), m_device(device) {}
 
+HipRenderer::HipRenderer(uint32_t spp, Camera* cam, Integrator* inte, std::vector<int> devices)
+    : Renderer(cam, inte), n_samples(spp), m_device(devices.empty() ? 0 : devices[0]), m_devices(std::move(devices)) {}
+
 HipRenderer::~HipRenderer() {
     if (m_ctx) xrt_destroy(m_ctx);
 }
@@ -23,7 +26,8 @@ void HipRenderer::render(const Scene& scene, Sampler::SamplerType, Image& image)
     m_status = XRT_OK;
     m_error.clear();
     if (!m_ctx) {
-        const int rc = xrt_create(m_device, &m_ctx);
+        const int rc = m_devices.size() > 1 ? xrt_create_multi(m_devices.data(), (int)m_devices.size(), &m_ctx)
+                                            : xrt_create(m_device, &m_ctx);
         if (rc != XRT_OK) return fail(rc, "xrt_create");
     }
     xrt_scene_desc desc;

@@ -11,6 +11,7 @@
 #include <cstring>
 #include <cfloat>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "bvh.h"
@@ -53,6 +54,10 @@ struct xrt_ctx {
     std::vector<hipEvent_t> events;
     hipEvent_t poll_ev[8] = {};  // live-count polls of render_impl (created once)
     hipEvent_t wait_ev = nullptr;   // xrt_render_device_after: the caller stream's position
+    // multi-GPU context (xrt_create_multi): one sub-context per device, each rendering an
+    // interleaved row shard; the frame is assembled in subs[0]'s framebuffer
+    std::vector<xrt_ctx*> subs;
+    DevBuf stage;              // multi: device-output staging on subs[0] (accumulate from a device image)
 };
 
 namespace {
@@ -137,6 +142,8 @@ int xrt_create(int device, xrt_ctx** out) {
 
 void xrt_destroy(xrt_ctx* c) {
     if (!c) return;
+    for (xrt_ctx* s : c->subs) xrt_destroy(s);
+    c->subs.clear();
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->tri, &c->tri_ng, &c->tri_nrm, &c->sph, &c->sph_obj, &c->box, &c->objs, &c->lights,
@@ -145,6 +152,7 @@ void xrt_destroy(xrt_ctx* c) {
                      &c->sample_k, &c->depth, &c->occ, &c->rng_c, &c->rng_g, &c->ring, &c->c_seg, &c->c_shadow,
                      &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch, &c->kparams};
     for (DevBuf* b : all) free_buf(*b);
+    free_buf(c->stage);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->poll_ev)
         if (e) (void)hipEventDestroy(e);
@@ -158,7 +166,7 @@ const char* xrt_last_error(const xrt_ctx* c) { return c ? c->err.c_str() : "no c
 
 // Flattened Scene -> device layout.  Primitives are re-packed in object iteration order,
 // so the linear scan order equals Scene::intersect's order (Src/scene.cpp:190-200).
-int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
+static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
     if (!c || !s) return XRT_ERR_INVALID;
     // a failed upload (OOM, bad range) must not leave the previous scene's freed buffers
     // behind a valid-looking context: renders are refused until an upload completes
@@ -375,7 +383,7 @@ int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
     return XRT_OK;
 }
 
-int xrt_set_camera(xrt_ctx* c, const float c2w[16], float scale, float aspect) {
+static int set_camera_one(xrt_ctx* c, const float c2w[16], float scale, float aspect) {
     if (!c || !c2w) return XRT_ERR_INVALID;
     std::memcpy(c->base.c2w, c2w, sizeof(float) * 16);
     c->base.scale = scale;
@@ -384,7 +392,7 @@ int xrt_set_camera(xrt_ctx* c, const float c2w[16], float scale, float aspect) {
     return XRT_OK;
 }
 
-int xrt_set_medium(xrt_ctx* c, const xrt_medium_desc* m) {
+static int set_medium_one(xrt_ctx* c, const xrt_medium_desc* m) {
     if (!c || !m) return XRT_ERR_INVALID;
     if (m->kind != XRT_MEDIUM_HETEROGENEOUS) {
         // HomogeneousMedium{MIS, Achromatic, NoMIS} (Src/medium.h:122-277): sigma_t = a + s
@@ -741,24 +749,178 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     return XRT_OK;
 }
 
+// ------------------------------------------------------------ multi-GPU context ----
+// ParallelRenderer::render fans the pixel loop out over the whole machine
+// (Src/renderer.cpp:83-99); here the machine is the listed GPUs.  Pixels are independent
+// (per-pixel seed and accumulation, Src/renderer.cpp:35-36,75), so device i renders the
+// interleaved rows y % (n * shard_count) == shard_index + shard_count * i — one host thread
+// and one HIP stream per device, all devices at once — and the frame is assembled in the
+// first device's framebuffer by one strided 2-D copy per other device (its own rows only,
+// over xGMI peer access): the same frame a zero-padded sum-reduce would produce, with 1/n
+// of the bytes and no arithmetic.  Bit-identical to the one-device render.
+int xrt_create_multi(const int* devices, int n_devices, xrt_ctx** out) {
+    if (!out) return XRT_ERR_INVALID;
+    *out = nullptr;
+    if (!devices || n_devices < 1 || n_devices > 64) return XRT_ERR_INVALID;
+    xrt_ctx* m = new xrt_ctx();
+    m->device = devices[0];
+    for (int i = 0; i < n_devices; ++i) {
+        xrt_ctx* s = nullptr;
+        const int rc = xrt_create(devices[i], &s);
+        if (rc != XRT_OK) {
+            xrt_destroy(m);
+            return rc;
+        }
+        m->subs.push_back(s);
+    }
+    // peer access from the first device to every other one (for the row gather); devices
+    // that cannot map each other fall back to the runtime's staged peer copy
+    (void)hipSetDevice(devices[0]);
+    for (int i = 1; i < n_devices; ++i) {
+        int can = 0;
+        if (devices[i] != devices[0] && hipDeviceCanAccessPeer(&can, devices[0], devices[i]) == hipSuccess && can) {
+            const hipError_t e = hipDeviceEnablePeerAccess(devices[i], 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+        }
+    }
+    *out = m;
+    return XRT_OK;
+}
+
+int xrt_device_count(const xrt_ctx* c) { return !c ? 0 : c->subs.empty() ? 1 : (int)c->subs.size(); }
+
+static int multi_fail(xrt_ctx* m, xrt_ctx* s, int rc, const char* what) {
+    return set_err(m, rc, std::string(what) + " on device " + std::to_string(s->device) + ": " + s->err);
+}
+
+int xrt_upload_scene(xrt_ctx* c, const xrt_scene_desc* s) {
+    if (!c || c->subs.empty()) return upload_scene_one(c, s);
+    for (xrt_ctx* d : c->subs) {
+        const int rc = upload_scene_one(d, s);
+        if (rc) return multi_fail(c, d, rc, "xrt_upload_scene");
+    }
+    return XRT_OK;
+}
+
+int xrt_set_camera(xrt_ctx* c, const float c2w[16], float scale, float aspect) {
+    if (!c || c->subs.empty()) return set_camera_one(c, c2w, scale, aspect);
+    for (xrt_ctx* d : c->subs) {
+        const int rc = set_camera_one(d, c2w, scale, aspect);
+        if (rc) return multi_fail(c, d, rc, "xrt_set_camera");
+    }
+    return XRT_OK;
+}
+
+int xrt_set_medium(xrt_ctx* c, const xrt_medium_desc* md) {
+    if (!c || c->subs.empty()) return set_medium_one(c, md);
+    for (xrt_ctx* d : c->subs) {
+        const int rc = set_medium_one(d, md);
+        if (rc) return multi_fail(c, d, rc, "xrt_set_medium");
+    }
+    return XRT_OK;
+}
+
+// d_out: the caller's device image on subs[0]'s GPU (or null: host image h_io).
+static int render_multi(xrt_ctx* m, const xrt_render_params* p, float* d_out, float* h_io, xrt_stats* st, int wait,
+                        hipStream_t wait_stream) {
+    const auto t_start = std::chrono::steady_clock::now();
+    if (!p) return set_err(m, XRT_ERR_INVALID, "null params");
+    if (p->width == 0 || p->height == 0 || p->shard_count == 0 || p->shard_index >= p->shard_count)
+        return set_err(m, XRT_ERR_INVALID, "bad image size or shard");
+    const uint32_t n = (uint32_t)m->subs.size();
+    const size_t npix = (size_t)p->width * p->height, bytes = npix * 3 * sizeof(float);
+    const bool acc = (p->flags & XRT_FLAG_ACCUMULATE) != 0;
+    xrt_ctx* s0 = m->subs[0];
+    HIPCHK(m, hipSetDevice(s0->device));
+    if (wait == 1) {
+        HIPCHK(m, hipDeviceSynchronize());
+    } else if (wait == 2) {
+        HIPCHK(m, hipEventRecord(s0->wait_ev, wait_stream));
+        HIPCHK(m, hipEventSynchronize(s0->wait_ev));
+    }
+    // every device renders into its own framebuffer; device 0 directly into the output
+    std::vector<float*> fbs(n, nullptr);
+    for (uint32_t i = 0; i < n; ++i) {
+        xrt_ctx* s = m->subs[i];
+        HIPCHK(m, hipSetDevice(s->device));
+        if (i == 0 && d_out) {
+            fbs[0] = d_out;
+        } else {
+            int rc = ensure(s, s->fb, bytes);
+            if (rc) return multi_fail(m, s, rc, "framebuffer");
+            fbs[i] = as<float>(s->fb);
+        }
+        if (acc) {   // each device starts its rows from the caller's image
+            if (d_out && i > 0)
+                HIPCHK(m, hipMemcpy(fbs[i], d_out, bytes, hipMemcpyDefault));
+            else if (!d_out)
+                HIPCHK(m, hipMemcpy(fbs[i], h_io, bytes, hipMemcpyHostToDevice));
+        }
+    }
+    std::vector<xrt_stats> S(n);
+    std::vector<int> rcs(n, XRT_OK);
+    std::vector<std::thread> th;
+    for (uint32_t i = 0; i < n; ++i) {
+        th.emplace_back([&, i] {
+            xrt_render_params q = *p;
+            q.shard_count = p->shard_count * n;
+            q.shard_index = p->shard_index + p->shard_count * i;
+            rcs[i] = render_impl(m->subs[i], &q, fbs[i], nullptr, &S[i]);
+        });
+    }
+    for (std::thread& t : th) t.join();
+    for (uint32_t i = 0; i < n; ++i)
+        if (rcs[i] != XRT_OK) return multi_fail(m, m->subs[i], rcs[i], "render");
+    // gather: device i's rows are y = shard_index + shard_count * (i + n * r)
+    HIPCHK(m, hipSetDevice(s0->device));
+    const size_t row = (size_t)p->width * 3 * sizeof(float), pitch = row * p->shard_count * n;
+    for (uint32_t i = 1; i < n; ++i) {
+        const uint32_t y0 = p->shard_index + p->shard_count * i;
+        if (y0 >= p->height) continue;
+        const uint32_t rows = (p->height - y0 + p->shard_count * n - 1) / (p->shard_count * n);
+        const size_t off = (size_t)y0 * row;
+        HIPCHK(m, hipMemcpy2DAsync(reinterpret_cast<char*>(fbs[0]) + off, pitch, reinterpret_cast<char*>(fbs[i]) + off,
+                                   pitch, row, rows, hipMemcpyDefault, s0->stream));
+    }
+    HIPCHK(m, hipStreamSynchronize(s0->stream));
+    if (h_io) HIPCHK(m, hipMemcpy(h_io, fbs[0], bytes, hipMemcpyDeviceToHost));
+    if (st) {
+        xrt_stats T = S[0];
+        for (uint32_t i = 1; i < n; ++i) {
+            for (int k = 0; k < XRT_K_COUNT; ++k) T.kernel_ms[k] += S[i].kernel_ms[k], T.launches[k] += S[i].launches[k];
+            T.samples += S[i].samples, T.segments += S[i].segments, T.shadow_rays += S[i].shadow_rays;
+            T.draws += S[i].draws, T.rejected += S[i].rejected, T.stalled += S[i].stalled;
+            T.path_slots += S[i].path_slots;
+            T.iterations = std::max(T.iterations, S[i].iterations);
+        }
+        T.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+        *st = T;
+    }
+    return XRT_OK;
+}
+
 int xrt_render(xrt_ctx* c, const xrt_render_params* p, float* rgb_out, xrt_stats* st) {
     if (!rgb_out) return set_err(c, XRT_ERR_INVALID, "null output");
+    if (c && !c->subs.empty()) return render_multi(c, p, nullptr, rgb_out, st, 0, nullptr);
     return render_impl(c, p, nullptr, rgb_out, st);
 }
 
 int xrt_render_device(xrt_ctx* c, const xrt_render_params* p, float* d_rgb_out, xrt_stats* st) {
     if (!d_rgb_out) return set_err(c, XRT_ERR_INVALID, "null output");
+    if (c && !c->subs.empty()) return render_multi(c, p, d_rgb_out, nullptr, st, 1, nullptr);
     return render_impl(c, p, d_rgb_out, nullptr, st, 1);
 }
 
 int xrt_render_device_after(xrt_ctx* c, const xrt_render_params* p, float* d_rgb_out, void* hip_stream,
                             xrt_stats* st) {
     if (!d_rgb_out) return set_err(c, XRT_ERR_INVALID, "null output");
+    if (c && !c->subs.empty()) return render_multi(c, p, d_rgb_out, nullptr, st, 2, (hipStream_t)hip_stream);
     return render_impl(c, p, d_rgb_out, nullptr, st, 2, (hipStream_t)hip_stream);
 }
 
 // ---------------------------------------------------------------- self-tests ----
 int xrt_test_rng(xrt_ctx* c, const uint32_t* seeds, uint32_t n_seeds, uint32_t skip, uint32_t n, float* out) {
+    if (c && !c->subs.empty()) c = c->subs[0];   // multi-GPU context: its first device
     if (!c || !seeds || !out) return XRT_ERR_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     DevBuf ds, dout, rings;
@@ -775,6 +937,7 @@ int xrt_test_rng(xrt_ctx* c, const uint32_t* seeds, uint32_t n_seeds, uint32_t s
 }
 
 int xrt_test_trig(xrt_ctx* c, const float* x, uint32_t n, float* out) {
+    if (c && !c->subs.empty()) c = c->subs[0];   // multi-GPU context: its first device
     if (!c || !x || !out) return XRT_ERR_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     DevBuf dx, dout;
@@ -789,6 +952,7 @@ int xrt_test_trig(xrt_ctx* c, const float* x, uint32_t n, float* out) {
 }
 
 int xrt_test_logexp(xrt_ctx* c, const float* x, uint32_t n, float* out) {
+    if (c && !c->subs.empty()) c = c->subs[0];   // multi-GPU context: its first device
     if (!c || !x || !out) return XRT_ERR_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     DevBuf dx, dout;
@@ -803,6 +967,7 @@ int xrt_test_logexp(xrt_ctx* c, const float* x, uint32_t n, float* out) {
 }
 
 int xrt_test_powf(xrt_ctx* c, const float* x, uint32_t n, float y, float* out) {
+    if (c && !c->subs.empty()) c = c->subs[0];   // multi-GPU context: its first device
     if (!c || !x || !out) return XRT_ERR_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     DevBuf dx, dout;
@@ -817,6 +982,7 @@ int xrt_test_powf(xrt_ctx* c, const float* x, uint32_t n, float y, float* out) {
 }
 
 int xrt_tonemap(xrt_ctx* c, const float* d_rgb, uint32_t n_pixels, float gamma, uint8_t* rgb8_out) {
+    if (c && !c->subs.empty()) c = c->subs[0];   // multi-GPU context: its first device
     if (!c || !rgb8_out) return XRT_ERR_INVALID;
     const float* src = d_rgb ? d_rgb : as<float>(c->fb);
     if (!src || (!d_rgb && (size_t)n_pixels * 3 * sizeof(float) > c->fb.bytes))
@@ -834,6 +1000,7 @@ int xrt_tonemap(xrt_ctx* c, const float* d_rgb, uint32_t n_pixels, float gamma, 
 }
 
 int xrt_test_trig_draw_domain(xrt_ctx* c, uint32_t first, uint32_t count, float* out_sin, float* out_cos, float* out_r) {
+    if (c && !c->subs.empty()) c = c->subs[0];   // multi-GPU context: its first device
     if (!c || !out_sin || !out_cos || !out_r) return XRT_ERR_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     DevBuf ds, dc, dr;
@@ -853,6 +1020,7 @@ int xrt_test_trig_draw_domain(xrt_ctx* c, uint32_t first, uint32_t count, float*
 
 // every 32-bit input: mode 0 rcp_rn vs 1/b, mode 1 div_const(x, c, rc) vs x / c (device_math.h)
 int xrt_test_fastdiv(xrt_ctx* c, uint32_t mode, float cst, float rc, uint64_t* n_bad, uint32_t* first_bad16) {
+    if (c && !c->subs.empty()) c = c->subs[0];   // multi-GPU context: its first device
     if (!c || !n_bad || !first_bad16) return XRT_ERR_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
     unsigned long long* d_n = nullptr;

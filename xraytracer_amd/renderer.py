@@ -17,14 +17,21 @@ from .scenes import SceneBundle
 
 
 class HipRenderer:
-    def __init__(self, spp: int, device: int = 0):
+    def __init__(self, spp: int, device: int = 0, devices=None):
+        """device: one GPU; devices: a list of GPUs rendered as one (xrt_create_multi —
+        row shards per GPU, frame assembled on devices[0])."""
         self.spp = int(spp)
         self._lib = abi.lib()
         ctx = C.c_void_p()
-        rc = self._lib.xrt_create(int(device), C.byref(ctx))
+        if devices is not None:
+            devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+            rc = self._lib.xrt_create_multi(devs, len(devices), C.byref(ctx))
+            what = f"xrt_create_multi(devices={list(devices)})"
+        else:
+            rc = self._lib.xrt_create(int(device), C.byref(ctx))
+            what = f"xrt_create(device={device})"
         if rc != 0:
-            raise abi.XrtError(f"xrt_create(device={device}) failed ({rc}): "
-                               f"{self._lib.xrt_last_error(None).decode()}")
+            raise abi.XrtError(f"{what} failed ({rc}): {self._lib.xrt_last_error(None).decode()}")
         self.ctx = ctx
         self.stats = None
         self._uploaded = None
