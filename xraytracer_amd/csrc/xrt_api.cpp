@@ -650,7 +650,8 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
                                    req_counts + (epoch & 1) * kMaxParts, step_visits, blocks, c->stream);
             });
             if (e != hipSuccess) return hip_err(c, e, "k_step");
-            if (it % step_refill == step_refill - 1) {
+            // the merged kernel refills its slots' rings itself (wave_refill)
+            if (!merged && it % step_refill == step_refill - 1) {
                 e = refill();
                 if (e != hipSuccess) return hip_err(c, e, "k_refill");
             }
