@@ -1028,6 +1028,21 @@ void orc_kat_onb(const float* n, float* t, float* b) {
 void orc_kat_lambert(orc_mt* m, const float* ng, const float* dpdu, const float* dpdv, float* wi, float* pdf) {
     st3(wi, lambert_sample_dir(ld3(ng), ld3(dpdu), ld3(dpdv), m, pdf));
 }
+void orc_kat_lambert_bxdf(orc_mt* m, const float* albedo, const float* ng, const float* dpdu, const float* dpdv,
+                          float* f, float* wi, float* pdf) {
+    xrt_object ob;
+    memset(&ob, 0, sizeof(ob));
+    ob.material = XRT_MAT_LAMBERT;
+    ob.albedo[0] = albedo[0], ob.albedo[1] = albedo[1], ob.albedo[2] = albedo[2];
+    st3(wi, lambert_sample_dir(ld3(ng), ld3(dpdu), ld3(dpdv), m, pdf));
+    st3(f, eval_bxdf(&ob));
+}
+void orc_kat_camera(const orc_camera* cam, float u, float v, float* o, float* d) {
+    v3 ro, rd;
+    camera_ray(cam, u, v, &ro, &rd);
+    st3(o, ro);
+    st3(d, rd);
+}
 int orc_kat_ray_tri(const float* o, const float* d, const float* v0, const float* v1, const float* v2, float* tuv) {
     float t = 0, u = 0, v = 0;
     int r = ray_tri(ld3(o), ld3(d), ld3(v0), ld3(v1), ld3(v2), &t, &u, &v);

@@ -69,6 +69,11 @@ void orc_kat_onb(const float* n, float* t, float* b);                     /* geo
 /* Lambert::sampleDir with SurfaceInfo{ng, dpdu, dpdv} (material.h:55-73): consumes 2 draws */
 void orc_kat_lambert(orc_mt* m, const float* ng, const float* dpdu, const float* dpdv,
                      float* wi, float* pdf);
+/* Lambert::sampleBxDF + evaluateBxDF (material.h:39-53): f = albedo / PI, 2 draws */
+void orc_kat_lambert_bxdf(orc_mt* m, const float* albedo, const float* ng, const float* dpdu, const float* dpdv,
+                          float* f, float* wi, float* pdf);
+/* PinholeCamera::sampleRay (camera.h:49-60) for sensor coordinates (u, v) */
+void orc_kat_camera(const orc_camera* cam, float u, float v, float* o, float* d);
 /* Mesh::rayTriangleIntersect (primitive.cpp:140-168): returns hit, writes t,u,v */
 int orc_kat_ray_tri(const float* o, const float* d, const float* v0, const float* v1,
                     const float* v2, float* tuv);

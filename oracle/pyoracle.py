@@ -61,6 +61,8 @@ def lib():
         l.orc_kat_normalize.argtypes = [f32p, f32p]
         l.orc_kat_onb.argtypes = [f32p, f32p, f32p]
         l.orc_kat_lambert.argtypes = [C.POINTER(OrcMT), f32p, f32p, f32p, f32p, f32p]
+        l.orc_kat_lambert_bxdf.argtypes = [C.POINTER(OrcMT)] + [f32p] * 7
+        l.orc_kat_camera.argtypes = [C.POINTER(OrcCamera), C.c_float, C.c_float, f32p, f32p]
         l.orc_kat_ray_tri.argtypes = [f32p] * 5 + [f32p]
         l.orc_kat_sphere.argtypes = [f32p, f32p, f32p, C.c_float, f32p]
         l.orc_kat_sphere_occluded.argtypes = [f32p, f32p, f32p, C.c_float, C.c_float]

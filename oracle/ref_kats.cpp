@@ -266,6 +266,87 @@ int main() {
         o.key("wl_pmf"); o.arr(pmf);
     }
 
+    // 8. The pinhole camera's ray direction, PinholeCamera::sampleRay's expression
+    //    (Src/camera.h:52-55) evaluated with the reference's own Matrix44f, multDirMatrix
+    //    (geometry.h:653-669) and normalize (geometry.cpp:13-16): camera.h itself includes
+    //    spdlog and is not buildable here, so only its one-line expression is repeated.
+    //    Cameras: the Cornell c2w (Src/examples/cornellbox.cpp:29), the C3/C5 translations,
+    //    and random rotation-like matrices.  Also Matrix44f::multDirMatrix (member).
+    {
+        Gen g(0xCA3E4Au);
+        std::vector<uint32_t> mats, in, dirs, mem;
+        std::vector<Matrix44f> ms = {Matrix44f(-1.0, 0, 0, 0, 0, 1.0, 0, 0, 0, 0, -1.0, 0, 278, 274.4, -750.0, 1),
+                                     Matrix44f(1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 4, 8, 1),
+                                     Matrix44f(1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 63.5f, 63.5f, 345.1f, 1)};
+        for (int k = 0; k < 5; ++k) {
+            Matrix44f m;
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) m[r][c] = g.uni(-1.0f, 1.0f);
+            for (int c = 0; c < 3; ++c) m[3][c] = g.uni(-500.0f, 500.0f);
+            ms.push_back(m);
+        }
+        const float scales[] = {0.57735026f, 0.41421357f, 1.0f};
+        const float aspects[] = {4.0f / 3.0f, 16.0f / 9.0f, 1.0f};
+        int mi = 0;
+        for (const Matrix44f& m : ms) {
+            for (int r = 0; r < 4; ++r)
+                for (int c = 0; c < 4; ++c) mats.push_back(bits(m[r][c]));
+            for (int k = 0; k < 128; ++k) {
+                const float u = g.uni(0.0f, 1.0f), v = g.uni(0.0f, 1.0f);
+                const float scale = scales[(mi + k) % 3], aspect = aspects[(mi + 2 * k) % 3];
+                in.push_back(bits(u));
+                in.push_back(bits(v));
+                in.push_back(bits(scale));
+                in.push_back(bits(aspect));
+                const Vec3f dir((2 * u - 1) * scale, (1 - 2 * v) * scale / aspect, -1);
+                push3(dirs, normalize(multDirMatrix(dir, m)));
+                Vec3f dm;
+                m.multDirMatrix(dir, dm);
+                push3(mem, dm);
+            }
+            ++mi;
+        }
+        o.key("cam_c2w"); o.arr(mats);
+        o.key("cam_in"); o.arr(in);
+        o.key("cam_dir"); o.arr(dirs);
+        o.key("cam_multdir_member"); o.arr(mem);
+    }
+
+    // 9. Lambert::evaluateBxDF and sampleBxDF (Src/material.h:39-53): the BSDF value
+    //    albedo / PI and the sampled direction + pdf through the Material interface
+    {
+        Gen g(0x1A3B5u);
+        UniformSampler smp;
+        smp.setSeed(777);
+        std::vector<uint32_t> in, f, wi, pdfs, ev;
+        for (int k = 0; k < 256; ++k) {
+            const Vec3f albedo = g.vec(0.0f, 1.0f);
+            SurfaceInfo si;
+            si.ng = normalize(g.vec(-1.0f, 1.0f));
+            orthonormalBasis(si.ng, si.dpdu, si.dpdv);
+            const Vec3f wo = normalize(g.vec(-1.0f, 1.0f));
+            push3(in, albedo);
+            push3(in, si.ng);
+            push3(in, si.dpdu);
+            push3(in, si.dpdv);
+            push3(in, wo);
+            Lambert lam(albedo);
+            const Material& mat = lam;
+            Vec3f w;
+            float pdf = 0.0f;
+            push3(f, mat.sampleBxDF(wo, si, smp, w, pdf));
+            push3(wi, w);
+            pdfs.push_back(bits(pdf));
+            push3(ev, mat.evaluateBxDF(wo, w, si));
+        }
+        o.key("bxdf_seed"); o.arr({777u});
+        o.key("bxdf_in"); o.arr(in);
+        o.key("bxdf_f"); o.arr(f);
+        o.key("bxdf_wi"); o.arr(wi);
+        o.key("bxdf_pdf"); o.arr(pdfs);
+        o.key("bxdf_eval"); o.arr(ev);
+    }
+
     o.s += "\n}\n";
     std::fputs(o.s.c_str(), stdout);
     return 0;

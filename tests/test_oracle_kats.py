@@ -179,3 +179,47 @@ def test_vpt_nee_oracle():
     assert np.all(np.isfinite(img)) and np.all(img >= 0) and img.max() > 0
     vpt, stv = pyoracle.render(s, 24, 18, 4, integrator="vpt")
     assert stv["shadow_rays"] == 0 and not np.array_equal(img, vpt)
+
+
+def test_camera_ray_direction(golden):
+    """PinholeCamera::sampleRay's direction (Src/camera.h:52-55) — multDirMatrix
+    (geometry.h:653-669) + normalize evaluated by the reference's own code — for the
+    Cornell, C3 and C5 cameras and random matrices; the origin is c2w row 3."""
+    lib = pyoracle.lib()
+    mats = f32(golden["cam_c2w"]).reshape(-1, 16)
+    inp = f32(golden["cam_in"]).reshape(len(mats), -1, 4)
+    ref = np.asarray(golden["cam_dir"], np.uint32).reshape(len(mats), -1, 3)
+    for mi, m in enumerate(mats):
+        cam = pyoracle.OrcCamera()
+        for i in range(16):
+            cam.c2w[i] = float(m[i])
+        for k in range(inp.shape[1]):
+            u, v, cam.scale, cam.aspect = (float(x) for x in inp[mi, k])
+            o = np.zeros(3, np.float32)
+            d = np.zeros(3, np.float32)
+            lib.orc_kat_camera(C.byref(cam), C.c_float(u), C.c_float(v), pyoracle.fp(o), pyoracle.fp(d))
+            assert np.array_equal(bits(d), ref[mi, k]), (mi, k)
+            assert np.array_equal(o, m[12:15])
+
+
+def test_lambert_bxdf_through_material_interface(golden):
+    """Lambert::sampleBxDF + evaluateBxDF (Src/material.h:39-53): f = albedo / PI per
+    channel, the sampled direction and pdf 1 / (2 PI)."""
+    lib = pyoracle.lib()
+    m = pyoracle.mt(golden["bxdf_seed"][0])
+    inp = f32(golden["bxdf_in"]).reshape(-1, 5, 3)
+    f_ref = np.asarray(golden["bxdf_f"], np.uint32).reshape(-1, 3)
+    wi_ref = np.asarray(golden["bxdf_wi"], np.uint32).reshape(-1, 3)
+    pdf_ref = np.asarray(golden["bxdf_pdf"], np.uint32)
+    ev_ref = np.asarray(golden["bxdf_eval"], np.uint32).reshape(-1, 3)
+    assert np.array_equal(f_ref, ev_ref)
+    for k in range(len(inp)):
+        alb, ng, dpdu, dpdv, _ = (np.ascontiguousarray(inp[k, q]) for q in range(5))
+        f = np.zeros(3, np.float32)
+        wi = np.zeros(3, np.float32)
+        pdf = np.zeros(1, np.float32)
+        lib.orc_kat_lambert_bxdf(C.byref(m), pyoracle.fp(alb), pyoracle.fp(ng), pyoracle.fp(dpdu), pyoracle.fp(dpdv),
+                                 pyoracle.fp(f), pyoracle.fp(wi), pyoracle.fp(pdf))
+        assert np.array_equal(bits(f), f_ref[k]), k
+        assert np.array_equal(bits(wi), wi_ref[k]), k
+        assert bits(pdf)[0] == pdf_ref[k]
