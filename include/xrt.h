@@ -221,6 +221,24 @@ int  xrt_render_device(xrt_ctx* ctx, const xrt_render_params* p, float* d_rgb_ou
 int  xrt_render_device_after(xrt_ctx* ctx, const xrt_render_params* p, float* d_rgb_out, void* hip_stream,
                              xrt_stats* st);
 
+/* ---- ray queries: Scene::intersect / Scene::occluded (Src/scene.cpp:190-211) ---------- */
+/* One IntersectInfo (Src/ray.h:23-39) as Scene::intersect leaves a fresh one. */
+typedef struct {
+    int32_t hit;             /* the query's return value                                   */
+    int32_t object;          /* hitObject: index in iteration order (-1: none)             */
+    int32_t primitive;       /* mesh hits: the object's triangle that set surfaceInfo, else -1 */
+    float t;                 /* IntersectInfo::t  (kInfinity = FLT_MAX when nothing wrote it) */
+    float t1;                /* IntersectInfo::t1 (medium boxes)                           */
+    float position[3], ng[3], ns[3], dpdu[3], dpdv[3];   /* SurfaceInfo                  */
+    float barycentric[2];    /* SurfaceInfo::barycentric (u, v) of that triangle           */
+} xrt_hit;
+enum { XRT_QUERY_INTERSECT = 0, XRT_QUERY_OCCLUDED = 1 };
+/* n rays rays[i] = {ox, oy, oz, dx, dy, dz} against the uploaded scene, on the GPU with the
+ * render's own trace kernels: XRT_QUERY_INTERSECT fills out[i] like Scene::intersect on a
+ * fresh IntersectInfo; XRT_QUERY_OCCLUDED sets out[i].hit = Scene::occluded(ray, tmax[i])
+ * (tmax NULL: FLT_MAX) and leaves the other fields zero.  Blocks until done. */
+int  xrt_query(xrt_ctx* ctx, uint32_t n, const float* rays, const float* tmax, int32_t mode, xrt_hit* out);
+
 /* Output stage: Image::gammaCorrection(gamma) then writePPM's 8-bit quantisation
  * (Src/image.h:80-114) on the device, for n_pixels float3 pixels: d_rgb is a DEVICE
  * pointer on this context's GPU, or NULL for the framebuffer of the last xrt_render;

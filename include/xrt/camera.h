@@ -1,8 +1,11 @@
 // xrt/camera.h — Camera / PinholeCamera (Src/camera.h:7-60).  The host computes
-// scale = tan(0.5*deg2rad(FOV)) exactly like the reference constructor; ray generation
-// runs on the GPU.
+// scale = tan(0.5*deg2rad(FOV)) exactly like the reference constructor; the renderer
+// generates its rays on the GPU (path_common.h camera_ray), and sampleRay is the same
+// expression for host code that asks the camera for a ray.
 #pragma once
 #include "geometry.h"
+#include "ray.h"
+#include "sampler.h"
 
 class Camera {
 public:
@@ -12,6 +15,8 @@ public:
     float aspectRatio() const { return aspect_ratio; }
     const Matrix44f& cameraToWorld() const { return camera2world; }
     virtual float scale() const = 0;
+    // sample a ray from sensor coordinates uv in [0, 1)^2 (Src/camera.h:28-30)
+    virtual bool sampleRay(const Vec2f& uv, Sampler& sampler, Ray& ray, float& pdf) const = 0;
 
 protected:
     float aspect_ratio;
@@ -30,6 +35,14 @@ public:
     PinholeCamera(float aspect_ratio_, const Matrix44f& c2w, float FOV = 90.0f)
         : Camera(aspect_ratio_, c2w), FOV_(FOV), scale_(pinhole_scale(FOV)) {}
     float scale() const override { return scale_; }
+    // PinholeCamera::sampleRay (Src/camera.h:49-60)
+    bool sampleRay(const Vec2f& pixel, Sampler&, Ray& ray, float& pdf) const override {
+        const Vec3f dir((2 * pixel[0] - 1) * scale_, (1 - 2 * pixel[1]) * scale_ / aspect_ratio, -1);
+        ray.direction = normalize(multDirMatrix(dir, camera2world));
+        ray.origin = Vec3f(camera2world[3][0], camera2world[3][1], camera2world[3][2]);
+        pdf = 1.0f;
+        return true;
+    }
 
 private:
     float FOV_;

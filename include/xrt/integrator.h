@@ -5,14 +5,40 @@
 // schedule; they do not integrate on the CPU.  Whitted (delta lights) is not provided.
 #pragma once
 #include <cstdint>
+#include <cstdio>
+#include <limits>
+
+#include "geometry.h"
+#include "ray.h"
+#include "sampler.h"
+
+class Scene;
 
 class Integrator {
 public:
-    enum class Kind { GI, Direct, VolumePathTracing, Indirect, Normal, VolumePathTracingNEE };
+    // Custom: a subclass written against the reference interface (default constructor +
+    // integrate override, Src/integrator.h:9-17).  HipRenderer renders the built-in kinds
+    // on the GPU and reports XRT_ERR_UNSUPPORTED for custom ones, which only a CPU
+    // renderer calling integrate() per sample can run.
+    enum class Kind { GI, Direct, VolumePathTracing, Indirect, Normal, VolumePathTracingNEE, Custom };
+    Integrator() : kind_(Kind::Custom), maxDepth_(0) {}
     explicit Integrator(Kind k, uint32_t maxDepth) : kind_(k), maxDepth_(maxDepth) {}
     virtual ~Integrator() = default;
     Kind kind() const { return kind_; }
     uint32_t maxDepth() const { return maxDepth_; }
+    // radiance along one ray (Src/integrator.h:14-16).  The built-in integrators run as GPU
+    // passes over whole frames (HipRenderer) and have no per-ray host form: called on one
+    // of them this logs once and returns NaN — the value the reference's renderer drops as
+    // a rejected sample (Src/renderer.cpp:57-73).  Custom integrators override it.
+    virtual Vec3f integrate(const Ray&, const Scene&, Sampler&) const {
+        static bool warned = false;
+        if (!warned) {
+            warned = true;
+            std::fprintf(stderr, "[xrt] Integrator::integrate: built-in integrators run on the GPU through "
+                                 "HipRenderer; no per-ray host integrate\n");
+        }
+        return Vec3f(std::numeric_limits<float>::quiet_NaN());
+    }
 
 private:
     Kind kind_;

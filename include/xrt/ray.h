@@ -1,6 +1,9 @@
-// xrt/ray.h — Ray and AABB (Src/ray.h:5-44).  SurfaceInfo/IntersectInfo are device-side
-// records in this build (xraytracer_amd/csrc/wavefront.h) and are not part of the host API.
+// xrt/ray.h — Ray, SurfaceInfo, IntersectInfo and AABB (Src/ray.h:5-44).  The renderer keeps
+// these records on the device; the host structs are what Scene::intersect fills
+// (a GPU query, xrt_query).
 #pragma once
+#include <cfloat>
+
 #include "geometry.h"
 
 class Ray {
@@ -12,6 +15,24 @@ public:
     Ray() {}
     Ray(const Vec3f& o, const Vec3f& d) : origin(o), direction(d) {}
     Vec3f operator()(float t) const { return origin + t * direction; }
+};
+
+struct SurfaceInfo {
+    Vec3f position;
+    Vec3f ng;      // geometric normal
+    Vec3f ns;      // shading normal
+    Vec3f dpdu;    // tangent vector
+    Vec3f dpdv;    // bitangent vector
+    Vec2f texcoords;
+    Vec2f barycentric;
+};
+
+class Object;
+struct IntersectInfo {
+    float t1 = FLT_MAX;   // [medium]: distance to the surface (kInfinity)
+    float t = FLT_MAX;    // distance to the hit point
+    SurfaceInfo surfaceInfo;
+    const Object* hitObject = nullptr;
 };
 
 struct AABB {

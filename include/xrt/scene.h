@@ -15,9 +15,14 @@
 #include "medium.h"
 #include "primitive.h"
 
+class Sampler;
+
 class Scene {
 public:
-    ~Scene() = default;
+    Scene() = default;
+    ~Scene();
+    Scene(const Scene&) = delete;
+    Scene& operator=(const Scene&) = delete;
     // Scene::loadObj (Src/scene.cpp:46-154) with tinyobjloader v2 parsing/triangulation;
     // returns false (and sets lastError) where the reference calls exit(1).
     bool loadObj(const std::string& filepath);
@@ -25,6 +30,18 @@ public:
     void build() {}
     void addAreaLight(std::string name, std::unique_ptr<AreaLight> light);
     const std::vector<std::unique_ptr<AreaLight>>& getAreaLights() const { return m_areaLights; }
+    // uniform choice among the area lights (Src/scene.cpp:182-188): one draw
+    const AreaLight* sampleAreaLight(Sampler& sampler, float& pdf) const;
+    // Scene::intersect / Scene::occluded (Src/scene.cpp:190-211), answered on the GPU by
+    // the renderer's own trace kernels (xrt_query on a context of device 0, created and
+    // uploaded on first use and after the scene changes).  `info` must be fresh (t = t1 =
+    // kInfinity), as at every call site of the reference; on a device error intersect /
+    // occluded return false and lastError() says why.
+    bool intersect(const Ray& ray, IntersectInfo& info) const;
+    bool occluded(const Ray& ray, float t_max) const;
+    // batched forms: one GPU pass for all rays
+    void intersect(const std::vector<Ray>& rays, std::vector<IntersectInfo>& infos, std::vector<char>& hits) const;
+    void occluded(const std::vector<Ray>& rays, const std::vector<float>& t_max, std::vector<char>& hits) const;
 
     // ---- additions for the GPU backend ----
     // Flattened, in m_objects iteration order; valid until the scene changes.
@@ -34,6 +51,7 @@ public:
     const Medium* anyMedium() const;
     const HeterogeneousMedium* medium() const;
     std::vector<std::string> objectNames() const;
+    int objectIndex(const Object* obj) const;   // position in iteration order, -1 if absent
     const std::string& lastError() const { return m_error; }
     // materials created by loadObj are owned here (Src/scene.h:46)
     Material* ownMaterial(std::unique_ptr<Material> m);
@@ -42,7 +60,14 @@ private:
     std::vector<std::unique_ptr<AreaLight>> m_areaLights;
     std::unordered_map<std::string, std::unique_ptr<Object>> m_objects;
     std::vector<std::unique_ptr<Material>> m_material;
-    std::string m_error;
+    mutable std::string m_error;
+    // ray queries: device context, scene version uploaded to it, objects in iteration order
+    uint64_t m_version = 0;
+    mutable uint64_t m_qversion = ~0ull;
+    mutable xrt_ctx* m_qctx = nullptr;
+    mutable std::vector<const Object*> m_order;
+    bool query(const float* rays, const float* tmax, uint32_t n, int mode, xrt_hit* out) const;
+    void fillInfo(const xrt_hit& h, IntersectInfo& info) const;
     // flatten() storage
     mutable std::vector<xrt_object> f_objects;
     mutable std::vector<float> f_triv, f_trin, f_sph, f_box;

@@ -132,6 +132,8 @@ typedef struct {
     float t1, t;
     v3 pos, ng, ns, dpdu, dpdv;
     int hit; /* object index, -1 = none (IntersectInfo::hitObject) */
+    int prim; /* the triangle (within its mesh) that last wrote barycentric, -1 = none */
+    float bu, bv; /* SurfaceInfo::barycentric */
 } hinfo;
 
 static inline void hinfo_init(hinfo* h) {
@@ -139,6 +141,7 @@ static inline void hinfo_init(hinfo* h) {
     h->t1 = K_INF;
     h->t = K_INF;
     h->hit = -1;
+    h->prim = -1;
 }
 
 typedef struct {
@@ -187,6 +190,7 @@ static int mesh_intersect(const xrt_scene_desc* S, int obj, v3 o, v3 d, hinfo* i
                                 vmuls(tri_nrm(S, i, 2), v));
                 onb(info->ns, &info->dpdu, &info->dpdv);
                 info->hit = obj;
+                info->prim = i - ob->first, info->bu = u, info->bv = v;
             }
         }
     }
@@ -1013,6 +1017,31 @@ int orc_trace_pixels(const xrt_scene_desc* S, const orc_camera* cam, const xrt_m
         uint64_t dr = 0, rj = 0;
         (void)do_render_pixel(&C, cam, p, pix_i[q], pix_j[q], &pc, &dr, &rj, rad + (size_t)q * p->spp * 3,
                               draws + (size_t)q * p->spp, segs + (size_t)q * p->spp, mk(0, 0, 0));
+    }
+    return XRT_OK;
+}
+
+/* Scene::intersect on a fresh IntersectInfo / Scene::occluded (Src/scene.cpp:190-211) for n
+ * rays {o, d} — the checker of xrt_query */
+int orc_query(const xrt_scene_desc* S, uint32_t n, const float* rays, const float* tmax, int mode, xrt_hit* out) {
+    uint64_t tests = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const float* r = rays + 6 * (size_t)i;
+        const v3 o = mk(r[0], r[1], r[2]), d = mk(r[3], r[4], r[5]);
+        xrt_hit* q = &out[i];
+        memset(q, 0, sizeof(*q));
+        q->object = -1, q->primitive = -1, q->t = K_INF, q->t1 = K_INF;
+        if (mode == XRT_QUERY_OCCLUDED) {
+            q->hit = scene_occluded(S, o, d, tmax ? tmax[i] : K_INF, &tests);
+            continue;
+        }
+        hinfo h;
+        hinfo_init(&h);
+        q->hit = scene_intersect(S, o, d, &h, &tests);
+        if (h.hit < 0) continue;
+        q->object = h.hit, q->primitive = h.prim, q->t = h.t, q->t1 = h.t1;
+        st3(q->position, h.pos), st3(q->ng, h.ng), st3(q->ns, h.ns), st3(q->dpdu, h.dpdu), st3(q->dpdv, h.dpdv);
+        if (h.prim >= 0) q->barycentric[0] = h.bu, q->barycentric[1] = h.bv;
     }
     return XRT_OK;
 }

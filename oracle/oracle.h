@@ -63,6 +63,10 @@ int orc_trace_pixels(const xrt_scene_desc* scene, const orc_camera* cam,
                      const uint32_t* pix_i, const uint32_t* pix_j, uint32_t n,
                      float* rad, uint32_t* draws, uint32_t* segs);
 
+/* Scene::intersect (fresh IntersectInfo) / Scene::occluded for n rays {o, d}: the checker
+ * of xrt_query, same record layout */
+int orc_query(const xrt_scene_desc* scene, uint32_t n, const float* rays, const float* tmax, int mode, xrt_hit* out);
+
 /* ---- building-block KATs (each mirrors one reference function) ---------------------- */
 void orc_kat_normalize(const float* v, float* out);                     /* geometry.cpp:13-16 */
 void orc_kat_onb(const float* n, float* t, float* b);                     /* geometry.cpp:43-49 */

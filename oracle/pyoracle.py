@@ -61,6 +61,7 @@ def lib():
         l.orc_kat_normalize.argtypes = [f32p, f32p]
         l.orc_kat_onb.argtypes = [f32p, f32p, f32p]
         l.orc_kat_lambert.argtypes = [C.POINTER(OrcMT), f32p, f32p, f32p, f32p, f32p]
+        l.orc_query.argtypes = [C.POINTER(abi.XrtSceneDesc), C.c_uint32, f32p, f32p, C.c_int, C.POINTER(abi.XrtHit)]
         l.orc_kat_lambert_bxdf.argtypes = [C.POINTER(OrcMT)] + [f32p] * 7
         l.orc_kat_camera.argtypes = [C.POINTER(OrcCamera), C.c_float, C.c_float, f32p, f32p]
         l.orc_kat_ray_tri.argtypes = [f32p] * 5 + [f32p]
@@ -182,3 +183,15 @@ def tonemap(img, gamma):
     lib().orc_tonemap(fp(a.reshape(-1)), a.size, float(gamma), out.ctypes.data_as(C.POINTER(C.c_uint8)))
     return out
 
+
+
+def query(scene, rays, tmax=None, occluded=False):
+    """Scene::intersect / Scene::occluded restated (checker of HipRenderer.query)."""
+    r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+    n = len(r)
+    out = (abi.XrtHit * max(1, n))()
+    tm = None if tmax is None else np.ascontiguousarray(np.broadcast_to(np.asarray(tmax, np.float32), (n,)))
+    rc = lib().orc_query(C.byref(scene.desc), n, fp(r), fp(tm) if tm is not None else None, 1 if occluded else 0, out)
+    if rc != 0:
+        raise RuntimeError(f"orc_query failed ({rc})")
+    return out[:n]

@@ -88,6 +88,15 @@ class XrtStats(C.Structure):
         return d
 
 
+class XrtHit(C.Structure):
+    _fields_ = [("hit", C.c_int32), ("object", C.c_int32), ("primitive", C.c_int32), ("t", C.c_float),
+                ("t1", C.c_float), ("position", C.c_float * 3), ("ng", C.c_float * 3), ("ns", C.c_float * 3),
+                ("dpdu", C.c_float * 3), ("dpdv", C.c_float * 3), ("barycentric", C.c_float * 2)]
+
+
+XRT_QUERY_INTERSECT, XRT_QUERY_OCCLUDED = 0, 1
+
+
 # Every symbol include/xrt.h declares, with its ctypes signature.
 SIGNATURES = {
     "xrt_abi_version": (C.c_int, []),
@@ -122,6 +131,7 @@ SIGNATURES = {
     "xrt_test_trig_draw_domain": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, f32p, f32p, f32p]),
     "xrt_test_logexp": (C.c_int, [C.c_void_p, f32p, C.c_uint32, f32p]),
     "xrt_test_powf": (C.c_int, [C.c_void_p, f32p, C.c_uint32, C.c_float, f32p]),
+    "xrt_query": (C.c_int, [C.c_void_p, C.c_uint32, f32p, f32p, C.c_int32, C.POINTER(XrtHit)]),
     "xrt_tonemap": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_float, C.POINTER(C.c_uint8)]),
     "xrt_test_fastdiv": (C.c_int, [C.c_void_p, C.c_uint32, C.c_float, C.c_float, C.POINTER(C.c_uint64), u32p]),
 }

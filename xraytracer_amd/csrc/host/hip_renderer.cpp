@@ -51,6 +51,8 @@ void HipRenderer::render(const Scene& scene, Sampler::SamplerType, Image& image)
         case Integrator::Kind::Indirect: p.integrator = XRT_INTEGRATOR_INDIRECT; break;
         case Integrator::Kind::Normal: p.integrator = XRT_INTEGRATOR_NORMAL; break;
         case Integrator::Kind::VolumePathTracingNEE: p.integrator = XRT_INTEGRATOR_VPT_NEE; break;
+        case Integrator::Kind::Custom:
+            return fail(XRT_ERR_UNSUPPORTED, "custom Integrator subclasses have no GPU form");
     }
     const HomogeneousMedium* hom = dynamic_cast<const HomogeneousMedium*>(scene.anyMedium());
     if ((p.integrator == XRT_INTEGRATOR_VPT || p.integrator == XRT_INTEGRATOR_VPT_NEE) && hom) {

@@ -12,6 +12,7 @@
 #include "xrt/grid.h"
 #include "xrt/image.h"
 #include "xrt/light.h"
+#include "xrt/sampler.h"
 #include "xrt/material.h"
 #include "xrt/medium.h"
 #include "xrt/primitive.h"
@@ -459,6 +460,7 @@ bool Scene::loadObj(const std::string& filepath) {
         // e.g. testdata/sphere32.obj); here the mesh gets no material.
         Material* mp = (materialID >= 0 && materialID < (int)matptr.size()) ? matptr[materialID] : nullptr;
         m_objects[sh.name] = std::make_unique<Mesh>(std::move(prims), mp, nullptr);
+        ++m_version;
     }
     (void)warn;
     return true;
@@ -469,11 +471,126 @@ Material* Scene::ownMaterial(std::unique_ptr<Material> m) {
     return m_material.back().get();
 }
 
-void Scene::addObj(std::string name, std::unique_ptr<Object> obj) { m_objects[name] = std::move(obj); }
+void Scene::addObj(std::string name, std::unique_ptr<Object> obj) {
+    m_objects[name] = std::move(obj);
+    ++m_version;
+}
+
+Scene::~Scene() {
+    if (m_qctx) xrt_destroy(m_qctx);
+}
+
+// Scene::sampleAreaLight (Src/scene.cpp:182-188)
+const AreaLight* Scene::sampleAreaLight(Sampler& sampler, float& pdf) const {
+    unsigned int lightIdx = m_areaLights.size() * sampler.getNext1D();
+    if (lightIdx == m_areaLights.size()) lightIdx--;
+    pdf = 1.0f / m_areaLights.size();
+    return m_areaLights[lightIdx].get();
+}
+
+// GPU ray queries (xrt_query): upload on first use and after any change to the objects
+bool Scene::query(const float* rays, const float* tmax, uint32_t n, int mode, xrt_hit* out) const {
+    int rc = XRT_OK;
+    if (!m_qctx && (rc = xrt_create(0, &m_qctx)) != XRT_OK) {
+        m_qctx = nullptr;
+        m_error = std::string("[Scene] ray query: xrt_create failed: ") + xrt_last_error(nullptr);
+        return false;
+    }
+    if (m_qversion != m_version) {
+        xrt_scene_desc desc;
+        if ((rc = flatten(&desc)) != XRT_OK || (rc = xrt_upload_scene(m_qctx, &desc)) != XRT_OK) {
+            m_error = std::string("[Scene] ray query: upload failed: ") + xrt_last_error(m_qctx);
+            return false;
+        }
+        m_order.clear();
+        for (const auto& kv : m_objects) m_order.push_back(kv.second.get());   // flatten's order
+        m_qversion = m_version;
+    }
+    if ((rc = xrt_query(m_qctx, n, rays, tmax, mode, out)) != XRT_OK) {
+        m_error = std::string("[Scene] ray query failed: ") + xrt_last_error(m_qctx);
+        return false;
+    }
+    return true;
+}
+
+void Scene::fillInfo(const xrt_hit& h, IntersectInfo& info) const {
+    if (h.object < 0) return;   // nothing wrote the fresh IntersectInfo
+    info.t = h.t;
+    info.t1 = h.t1;
+    SurfaceInfo& s = info.surfaceInfo;
+    s.position = Vec3f(h.position[0], h.position[1], h.position[2]);
+    s.ng = Vec3f(h.ng[0], h.ng[1], h.ng[2]);
+    s.ns = Vec3f(h.ns[0], h.ns[1], h.ns[2]);
+    s.dpdu = Vec3f(h.dpdu[0], h.dpdu[1], h.dpdu[2]);
+    s.dpdv = Vec3f(h.dpdv[0], h.dpdv[1], h.dpdv[2]);
+    info.hitObject = (size_t)h.object < m_order.size() ? m_order[h.object] : nullptr;
+    if (h.primitive >= 0) {
+        const float u = h.barycentric[0], v = h.barycentric[1];
+        s.barycentric = Vec2f(u, v);
+        // texcoords[0] * (1 - u - v) + texcoords[1] * u + texcoords[2] * v (Src/primitive.cpp:104)
+        const Mesh* mesh = dynamic_cast<const Mesh*>(info.hitObject);
+        if (mesh && (size_t)h.primitive < mesh->primitives().size()) {
+            const std::vector<Vec2f>& tc = mesh->primitives()[h.primitive].texcoords();
+            if (tc.size() >= 3) {
+                const float w = 1.0f - u - v;
+                s.texcoords = Vec2f(tc[0][0] * w + tc[1][0] * u + tc[2][0] * v, tc[0][1] * w + tc[1][1] * u + tc[2][1] * v);
+            }
+        }
+    }
+}
+
+bool Scene::intersect(const Ray& ray, IntersectInfo& info) const {
+    const float r[6] = {ray.origin[0], ray.origin[1], ray.origin[2], ray.direction[0], ray.direction[1], ray.direction[2]};
+    xrt_hit h;
+    if (!query(r, nullptr, 1, XRT_QUERY_INTERSECT, &h)) return false;
+    fillInfo(h, info);
+    return h.hit != 0;
+}
+
+bool Scene::occluded(const Ray& ray, float t_max) const {
+    const float r[6] = {ray.origin[0], ray.origin[1], ray.origin[2], ray.direction[0], ray.direction[1], ray.direction[2]};
+    xrt_hit h;
+    return query(r, &t_max, 1, XRT_QUERY_OCCLUDED, &h) && h.hit != 0;
+}
+
+void Scene::intersect(const std::vector<Ray>& rays, std::vector<IntersectInfo>& infos, std::vector<char>& hits) const {
+    const size_t n = rays.size();
+    std::vector<float> r(6 * n);
+    for (size_t i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) r[6 * i + k] = rays[i].origin[k], r[6 * i + 3 + k] = rays[i].direction[k];
+    std::vector<xrt_hit> h(n);
+    infos.assign(n, IntersectInfo());
+    hits.assign(n, 0);
+    if (n == 0 || !query(r.data(), nullptr, (uint32_t)n, XRT_QUERY_INTERSECT, h.data())) return;
+    for (size_t i = 0; i < n; ++i) {
+        fillInfo(h[i], infos[i]);
+        hits[i] = h[i].hit != 0;
+    }
+}
+
+void Scene::occluded(const std::vector<Ray>& rays, const std::vector<float>& t_max, std::vector<char>& hits) const {
+    const size_t n = rays.size();
+    std::vector<float> r(6 * n);
+    for (size_t i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) r[6 * i + k] = rays[i].origin[k], r[6 * i + 3 + k] = rays[i].direction[k];
+    std::vector<xrt_hit> h(n);
+    hits.assign(n, 0);
+    if (n == 0 || t_max.size() < n || !query(r.data(), t_max.data(), (uint32_t)n, XRT_QUERY_OCCLUDED, h.data())) return;
+    for (size_t i = 0; i < n; ++i) hits[i] = h[i].hit != 0;
+}
 
 void Scene::addAreaLight(std::string name, std::unique_ptr<AreaLight> light) {
     addObj(name, light->makeObject());  // Src/scene.cpp:166-170
     m_areaLights.push_back(std::move(light));
+}
+
+int Scene::objectIndex(const Object* obj) const {
+    int i = 0;
+    for (const auto& kv : m_objects) {
+        if (kv.second.get() == obj) return i;
+        ++i;
+    }
+    return -1;
 }
 
 std::vector<std::string> Scene::objectNames() const {

@@ -48,6 +48,10 @@ hipError_t launch_step_merged(const KParams& P, const KParams* dP, const StepObj
 // the merged schedule's refill (leaves ST_RNGREQ to the merged kernel; see step_tri.hip)
 hipError_t launch_refill_merged(const KParams& P, const uint32_t* count, uint32_t* zero_count, hipStream_t st);
 hipError_t launch_finish(const KParams& P, hipStream_t st);
+// Scene::intersect / occluded for n = P.n_slots caller rays (xrt_query): rays [n][6] on the
+// device, tmax [n] or null; list / count (one partition) / zero are scratch
+hipError_t launch_query(const KParams& P, const float* rays, const float* tmax, int mode, uint32_t* list,
+                        uint32_t* count, uint32_t* zero, xrt_hit* out, hipStream_t st);
 hipError_t launch_test_rng(const uint32_t* seeds, uint32_t n_seeds, uint32_t skip, uint32_t n, float* out,
                            uint32_t* rings, hipStream_t st);
 hipError_t launch_test_trig(const float* x, uint32_t n, float* out, hipStream_t st);

@@ -2270,6 +2270,84 @@ hipError_t launch_step(const KParams& P, const KParams* dP, const uint32_t* list
     }
 }
 
+// ------------------------------------------------------------------ ray queries ----
+// Scene::intersect / Scene::occluded for caller rays (xrt_query): the rays become the slots
+// of a one-partition list, launch_trace (the render's own trace kernels, BVHs included)
+// writes the hit records, and k_query_out rebuilds IntersectInfo with the shading code's
+// surface() — the same records the integrators read.
+__global__ __launch_bounds__(kBlock) void k_query_in(KParams P, const float* __restrict__ rays,
+                                                     const float* __restrict__ tmax, int mode, uint32_t* list,
+                                                     uint32_t* count) {
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    if (s == 0) count[0] = P.n_slots;
+    if (s >= P.n_slots) return;
+    const float* r = rays + 6 * (size_t)s;
+    list[s] = s;
+    P.occ[s] = 0;
+    if (mode == XRT_QUERY_INTERSECT) {
+        P.ray_o[s] = make_float4(r[0], r[1], r[2], 0.0f);
+        P.ray_d[s] = make_float4(r[3], r[4], r[5], 0.0f);
+        P.state[s] = ST_RAY;
+    } else {
+        P.sh_o[s] = make_float4(r[0], r[1], r[2], tmax ? tmax[s] : kINF);
+        P.sh_d[s] = make_float4(r[3], r[4], r[5], 0.0f);
+        P.state[s] = 1u << ST_SHADOW_SHIFT;
+    }
+}
+
+template <int SCN>
+__global__ __launch_bounds__(kBlock) void k_query_out(KParams P, int mode, xrt_hit* __restrict__ out) {
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= P.n_slots) return;
+    xrt_hit q;
+    memset(&q, 0, sizeof(q));
+    q.object = -1, q.primitive = -1;
+    if (mode != XRT_QUERY_INTERSECT) {
+        q.hit = P.occ[s] & 1u;
+        q.t = q.t1 = kINF;
+        out[s] = q;
+        return;
+    }
+    const v3 o = xyz(P.ray_o[s]), d = xyz(P.ray_d[s]);
+    const f4 h = P.hit[s];
+    Surf S;
+    float t1;
+    const int obj = surface<SCN>(P, s, o, d, h, S, t1);
+    // the triangle that last wrote barycentric (with dpdu / dpdv; spheres and boxes leave
+    // both untouched), and its (u, v)
+    int surf = SCN == SCN_SPHERE ? -1 : __float_as_int(h.w);
+    float su = h.y, sv = h.z;
+    if (SCN == SCN_MIXED && surf >= 0) {
+        const f4 h2 = P.hit2[s], h3 = P.hit3[s];
+        surf = __float_as_int(h2.z), su = h3.z, sv = h3.w;
+    }
+    q.hit = obj >= 0;
+    q.object = obj;
+    q.primitive = (surf >= 0 && (surf >> 28) == SEG_TRI) ? (surf & 0x0fffffff) : -1;   // global; host makes it local
+    q.t = obj >= 0 ? h.x : kINF;
+    q.t1 = t1;
+    const v3 f[5] = {S.pos, S.ng, S.ns, S.dpdu, S.dpdv};
+    float* dst[5] = {q.position, q.ng, q.ns, q.dpdu, q.dpdv};
+    for (int k = 0; k < 5; ++k) dst[k][0] = f[k].x, dst[k][1] = f[k].y, dst[k][2] = f[k].z;
+    if (q.primitive >= 0) q.barycentric[0] = su, q.barycentric[1] = sv;
+    out[s] = q;
+}
+
+hipError_t launch_query(const KParams& P, const float* rays, const float* tmax, int mode, uint32_t* list,
+                        uint32_t* count, uint32_t* zero, xrt_hit* out, hipStream_t st) {
+    const uint32_t blocks = (P.n_slots + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_query_in, dim3(blocks), dim3(kBlock), 0, st, P, rays, tmax, mode, list, count);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = launch_trace(P, list, count, zero, blocks, st);
+    if (e != hipSuccess) return e;
+    switch (P.scene_kind) {
+        case SCN_TRI: hipLaunchKernelGGL(k_query_out<SCN_TRI>, dim3(blocks), dim3(kBlock), 0, st, P, mode, out); break;
+        case SCN_SPHERE: hipLaunchKernelGGL(k_query_out<SCN_SPHERE>, dim3(blocks), dim3(kBlock), 0, st, P, mode, out); break;
+        default: hipLaunchKernelGGL(k_query_out<SCN_MIXED>, dim3(blocks), dim3(kBlock), 0, st, P, mode, out); break;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_finish(const KParams& P, hipStream_t st) {
     const uint32_t blocks = std::min<uint32_t>((P.n_slots + kBlock - 1) / kBlock, 2048u);
     hipLaunchKernelGGL(k_finish, dim3(blocks), dim3(kBlock), 0, st, P);

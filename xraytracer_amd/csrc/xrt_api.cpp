@@ -57,6 +57,10 @@ struct xrt_ctx {
     // multi-GPU context (xrt_create_multi): one sub-context per device, each rendering an
     // interleaved row shard; the frame is assembled in subs[0]'s framebuffer
     std::vector<xrt_ctx*> subs;
+    // ray queries (xrt_query): per object, its first triangle in the device arrays (-1: not
+    // a mesh), and the query's own buffers
+    std::vector<int> obj_tri_first;
+    DevBuf q_rays, q_tmax, q_out;
     DevBuf stage;              // multi: device-output staging on subs[0] (accumulate from a device image)
 };
 
@@ -152,7 +156,7 @@ void xrt_destroy(xrt_ctx* c) {
                      &c->sample_k, &c->depth, &c->occ, &c->rng_c, &c->rng_g, &c->ring, &c->c_seg, &c->c_shadow,
                      &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch, &c->kparams};
     for (DevBuf* b : all) free_buf(*b);
-    free_buf(c->stage);
+    free_buf(c->stage), free_buf(c->q_rays), free_buf(c->q_tmax), free_buf(c->q_out);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->poll_ev)
         if (e) (void)hipEventDestroy(e);
@@ -180,6 +184,7 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
     std::vector<int> sph_obj;
     std::vector<DObj> objs;
     std::vector<DSeg> segs;
+    std::vector<int> tri_first(s->n_objects, -1);
     auto V = [](const float* p) { return Vec3f(p[0], p[1], p[2]); };
     auto F4 = [](const Vec3f& v, float w) { return f4{v[0], v[1], v[2], w}; };
     auto bits = [](int x) { float f; std::memcpy(&f, &x, 4); return f; };
@@ -198,6 +203,7 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
                 return set_err(c, XRT_ERR_INVALID, "mesh range out of bounds");
             kind = SEG_TRI;
             first = (int)(tri.size() / 3);
+            tri_first[k] = first;
             for (int t = o.first; t < o.first + o.count; ++t) {
                 const float* v = s->tri_v + 9 * (size_t)t;
                 const float* n = s->tri_n + 9 * (size_t)t;
@@ -379,6 +385,7 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
         P.snode = as<f4>(c->snode), P.ssph = as<f4>(c->ssph), P.sbk = as<int>(c->sbk);
         P.n_snode = (int)T.size();
     }
+    c->obj_tri_first = std::move(tri_first);
     c->has_scene = true;
     return XRT_OK;
 }
@@ -896,6 +903,44 @@ static int render_multi(xrt_ctx* m, const xrt_render_params* p, float* d_out, fl
         }
         T.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
         *st = T;
+    }
+    return XRT_OK;
+}
+
+// Scene::intersect / Scene::occluded (Src/scene.cpp:190-211) for caller rays, on the GPU
+int xrt_query(xrt_ctx* c, uint32_t n, const float* rays, const float* tmax, int32_t mode, xrt_hit* out) {
+    if (c && !c->subs.empty()) c = c->subs[0];   // multi-GPU context: its first device
+    if (!c || (n && (!rays || !out))) return XRT_ERR_INVALID;
+    if (mode != XRT_QUERY_INTERSECT && mode != XRT_QUERY_OCCLUDED) return set_err(c, XRT_ERR_INVALID, "bad query mode");
+    if (!c->has_scene) return set_err(c, XRT_ERR_STATE, "upload a scene first");
+    if (n == 0) return XRT_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = ensure(c, c->ray_o, n * 16)) || (rc = ensure(c, c->ray_d, n * 16)) || (rc = ensure(c, c->hit, n * 16)) ||
+        (rc = ensure(c, c->hit2, n * 16)) || (rc = ensure(c, c->hit3, n * 16)) || (rc = ensure(c, c->sh_o, n * 16)) ||
+        (rc = ensure(c, c->sh_d, n * 16)) || (rc = ensure(c, c->state, n * 4)) || (rc = ensure(c, c->occ, n * 4)) ||
+        (rc = ensure(c, c->lists, (n + 64) * 4)) || (rc = ensure(c, c->counts, 5 * kMaxParts * 4)) ||
+        (rc = ensure(c, c->q_rays, (size_t)n * 24)) || (rc = ensure(c, c->q_tmax, (size_t)n * 4)) ||
+        (rc = ensure(c, c->q_out, (size_t)n * sizeof(xrt_hit))))
+        return rc;
+    // (buffers only ever grow, so the render's cap_slots invariant still holds)
+    KParams P = c->base;
+    P.n_slots = n, P.n_part = 1, P.part_cap = n;
+    P.ray_o = as<f4>(c->ray_o), P.ray_d = as<f4>(c->ray_d), P.hit = as<f4>(c->hit), P.hit2 = as<f4>(c->hit2);
+    P.hit3 = as<f4>(c->hit3), P.sh_o = as<f4>(c->sh_o), P.sh_d = as<f4>(c->sh_d);
+    P.state = as<uint32_t>(c->state), P.occ = as<uint32_t>(c->occ);
+    HIPCHK(c, hipMemcpyAsync(c->q_rays.p, rays, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+    if (tmax) HIPCHK(c, hipMemcpyAsync(c->q_tmax.p, tmax, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+    uint32_t* cnt = as<uint32_t>(c->counts);
+    HIPCHK(c, launch_query(P, as<float>(c->q_rays), tmax ? as<float>(c->q_tmax) : nullptr, mode, as<uint32_t>(c->lists),
+                           cnt, cnt + kMaxParts, as<xrt_hit>(c->q_out), c->stream));
+    HIPCHK(c, hipMemcpyAsync(out, c->q_out.p, (size_t)n * sizeof(xrt_hit), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (uint32_t i = 0; i < n; ++i) {   // the triangle within its object's mesh
+        xrt_hit& q = out[i];
+        if (q.primitive >= 0 && q.object >= 0 && (size_t)q.object < c->obj_tri_first.size() &&
+            c->obj_tri_first[q.object] >= 0)
+            q.primitive -= c->obj_tri_first[q.object];
     }
     return XRT_OK;
 }

@@ -94,6 +94,21 @@ class HipRenderer:
         self.stats = st
         return img
 
+    def query(self, scene: SceneBundle, rays: np.ndarray, tmax=None, occluded: bool = False):
+        """Scene::intersect (or, with occluded=True, Scene::occluded(ray, tmax)) for rays
+        (n, 6) = origin, direction, on the GPU with the render's trace kernels (xrt_query).
+        Returns an array of abi.XrtHit."""
+        if self._uploaded is not scene:
+            self.upload(scene)
+        r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+        n = len(r)
+        out = (abi.XrtHit * max(1, n))()
+        tm = None if tmax is None else np.ascontiguousarray(np.broadcast_to(np.asarray(tmax, np.float32), (n,)))
+        self._check(self._lib.xrt_query(self.ctx, n, abi.fptr(r), abi.fptr(tm) if tm is not None else None,
+                                        abi.XRT_QUERY_OCCLUDED if occluded else abi.XRT_QUERY_INTERSECT, out),
+                    "xrt_query")
+        return out[:n]
+
     def tonemap(self, width: int, height: int, gamma: float, device_ptr: int = 0) -> np.ndarray:
         """Image::gammaCorrection(gamma) + writePPM's 8-bit quantisation on the GPU, of the
         last render() (device_ptr 0) or of a device float3 buffer: (H, W, 3) uint8."""
