@@ -5,12 +5,14 @@
 // image; the density comes from a raw float file instead, in a DenseGrid with OpenVDB's
 // BoxSampler semantics.
 //
-//   nee grid.raw nx ny nz origin_x origin_y origin_z voxel [width height spp out.raw]
+//   nee grid.raw nx ny nz origin_x origin_y origin_z voxel [width height spp out.raw [sparse]]
 // grid.raw holds nz*ny*nx float32 ([z][y][x]); out.raw receives the linear framebuffer
 // (height*width*3 float32; default nee.ppm, gamma 2.2, like the reference example).
+// "sparse" stores the density as 8^3 leaf bricks (SparseGrid, the NanoVDB layout) instead.
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
+#include <string>
 #include <vector>
 
 #include <xrt/camera.h>
@@ -50,7 +52,12 @@ int main(int argc, char** argv) {
     const auto camera = std::make_unique<PinholeCamera>(aspect_ratio, c2w, FOV);
 
     Scene scene;
-    auto gridData = std::make_unique<DenseGrid>(nx, ny, nz, std::move(density), origin, voxel);
+    const bool sparse = argc > 13 && std::string(argv[13]) == "sparse";
+    std::unique_ptr<DensityGrid> gridData;
+    if (sparse)
+        gridData = std::make_unique<SparseGrid>(SparseGrid::fromDense(nx, ny, nz, density, origin, voxel));
+    else
+        gridData = std::make_unique<DenseGrid>(nx, ny, nz, std::move(density), origin, voxel);
     const auto medium = std::make_unique<HeterogeneousMedium>(0.0f, gridData.get(), Vec3f(0.01f), Vec3f(0.05f));
     scene.addObj("medium", medium->makeObject());
     const Matrix44<float> xfm_sphere(1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 400.0, 0.0, 1);

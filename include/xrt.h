@@ -205,6 +205,22 @@ int  xrt_upload_scene(xrt_ctx* ctx, const xrt_scene_desc* scene);
  * PinholeCamera::scale = tan(0.5*deg2rad(FOV)) and aspect_ratio (Src/camera.h:37-47) */
 int  xrt_set_camera(xrt_ctx* ctx, const float c2w[16], float scale, float aspect);
 int  xrt_set_medium(xrt_ctx* ctx, const xrt_medium_desc* medium);
+/* Sparse heterogeneous density in leaf bricks (the layout NanoVDB / OpenVDB give a grid:
+ * 8^3-voxel leaves, Src/examples/nanovdb_convert.cpp, Src/grid.h:22-83).  The grid's
+ * index space [0, nx) x [0, ny) x [0, nz) is cut into XRT_BRICK^3 bricks;
+ * table[(bz * nby + by) * nbx + bx] is the brick's index in `bricks` or -1 (inactive:
+ * background 0, as OpenVDB's BoxSampler reads it).  bricks[b] holds XRT_BRICK^3 floats in
+ * [z][y][x] order.  Sampling is the same trilinear BoxSampler as the dense grid, so a brick
+ * grid renders bit-identically to the dense grid it was cut from.  medium->density is
+ * ignored; every other field of xrt_medium_desc keeps its meaning. */
+#define XRT_BRICK 8
+typedef struct {
+    uint32_t nbx, nby, nbz;      /* bricks per axis: ceil(n / XRT_BRICK)                    */
+    const int32_t* table;        /* [nbz][nby][nbx] brick index or -1                        */
+    uint32_t n_bricks;
+    const float* bricks;         /* [n_bricks][XRT_BRICK^3]                                  */
+} xrt_brick_grid;
+int  xrt_set_medium_bricks(xrt_ctx* ctx, const xrt_medium_desc* medium, const xrt_brick_grid* grid);
 
 /* Render into caller-owned HOST memory rgb_out[height][width][3] (Image::pixels order
  * j + width*i).  Pixels outside this shard are written as 0.  Blocks until done. */

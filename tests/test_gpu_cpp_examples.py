@@ -47,7 +47,8 @@ def test_vpt_example_homogeneous_mis(tmp_path):
     assert np.array_equal(img, ref), np.argwhere(~np.all(img == ref, axis=-1))[:5]
 
 
-def test_nee_example_heterogeneous_dense_grid(tmp_path):
+@pytest.mark.parametrize("layout", ["dense", "sparse"])
+def test_nee_example_heterogeneous_dense_grid(tmp_path, layout):
     """HeterogeneousMedium over a DenseGrid + SphereLight(r 50, at y 400 through its
     lightToWorld), VolumePathTracingNEE(32), camera at (0, 70, 550), FOV 60: delta tracking,
     NEE ratio tracking, cone sampling of the sphere light."""
@@ -57,7 +58,7 @@ def test_nee_example_heterogeneous_dense_grid(tmp_path):
     gpath = tmp_path / "grid.raw"
     np.ascontiguousarray(grid, dtype=np.float32).tofile(gpath)
     out = tmp_path / "nee.raw"
-    run("nee", [gpath, n, n, n, *origin, voxel, w, h, spp, out])
+    run("nee", [gpath, n, n, n, *origin, voxel, w, h, spp, out, layout])
     img = np.fromfile(out, dtype=np.float32).reshape(h, w, 3)
     s = scenes.SceneBundle()
     s.add_medium("medium", scenes.Medium(grid, origin, voxel, 0.0, (0.01, 0.01, 0.01), (0.05, 0.05, 0.05)))

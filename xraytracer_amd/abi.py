@@ -66,6 +66,14 @@ class XrtMediumDesc(C.Structure):
                 ("density_multiplier", C.c_float), ("kind", C.c_int32)]
 
 
+class XrtBrickGrid(C.Structure):
+    _fields_ = [("nbx", C.c_uint32), ("nby", C.c_uint32), ("nbz", C.c_uint32), ("table", C.POINTER(C.c_int32)),
+                ("n_bricks", C.c_uint32), ("bricks", f32p)]
+
+
+XRT_BRICK = 8
+
+
 class XrtRenderParams(C.Structure):
     _fields_ = [("integrator", C.c_int32), ("max_depth", C.c_uint32), ("width", C.c_uint32),
                 ("height", C.c_uint32), ("spp", C.c_uint32), ("shard_index", C.c_uint32),
@@ -108,6 +116,7 @@ SIGNATURES = {
     "xrt_upload_scene": (C.c_int, [C.c_void_p, C.POINTER(XrtSceneDesc)]),
     "xrt_set_camera": (C.c_int, [C.c_void_p, f32p, C.c_float, C.c_float]),
     "xrt_set_medium": (C.c_int, [C.c_void_p, C.POINTER(XrtMediumDesc)]),
+    "xrt_set_medium_bricks": (C.c_int, [C.c_void_p, C.POINTER(XrtMediumDesc), C.POINTER(XrtBrickGrid)]),
     "xrt_render": (C.c_int, [C.c_void_p, C.POINTER(XrtRenderParams), f32p, C.POINTER(XrtStats)]),
     "xrt_render_device": (C.c_int, [C.c_void_p, C.POINTER(XrtRenderParams), C.c_void_p, C.POINTER(XrtStats)]),
     "xrt_render_device_after": (C.c_int, [C.c_void_p, C.POINTER(XrtRenderParams), C.c_void_p, C.c_void_p,

@@ -72,24 +72,34 @@ void HipRenderer::render(const Scene& scene, Sampler::SamplerType, Image& image)
     } else if (p.integrator == XRT_INTEGRATOR_VPT || p.integrator == XRT_INTEGRATOR_VPT_NEE) {
         const HeterogeneousMedium* med = scene.medium();
         const DenseGrid* grid = med ? dynamic_cast<const DenseGrid*>(med->grid()) : nullptr;
-        if (!grid) return fail(XRT_ERR_UNSUPPORTED, "VolumePathTracing needs a HeterogeneousMedium over a DenseGrid");
+        const SparseGrid* sparse = med ? dynamic_cast<const SparseGrid*>(med->grid()) : nullptr;
+        if (!grid && !sparse)
+            return fail(XRT_ERR_UNSUPPORTED, "VolumePathTracing needs a HeterogeneousMedium over a DenseGrid or SparseGrid");
         xrt_medium_desc md;
         std::memset(&md, 0, sizeof(md));
-        md.nx = grid->nx(), md.ny = grid->ny(), md.nz = grid->nz();
-        md.density = grid->data().data();
-        const AABB b = grid->getBounds();
+        md.nx = grid ? grid->nx() : sparse->nx(), md.ny = grid ? grid->ny() : sparse->ny();
+        md.nz = grid ? grid->nz() : sparse->nz();
+        const AABB b = med->grid()->getBounds();
+        const Vec3f& origin = grid ? grid->origin() : sparse->origin();
         for (int c = 0; c < 3; ++c) {
-            md.origin[c] = grid->origin()[c];
+            md.origin[c] = origin[c];
             md.bbox_min[c] = b.pMin[c];
             md.bbox_max[c] = b.pMax[c];
             md.absorption[c] = med->absorptionColor()[c];
             md.scattering[c] = med->scatteringColor()[c];
         }
-        md.voxel_size = grid->voxelSize();
-        md.max_density = grid->getMaxDensity();
+        md.voxel_size = grid ? grid->voxelSize() : sparse->voxelSize();
+        md.max_density = med->grid()->getMaxDensity();
         md.g = med->g();
         md.density_multiplier = med->densityMultiplier();
-        if ((rc = xrt_set_medium(m_ctx, &md)) != XRT_OK) return fail(rc, "xrt_set_medium");
+        if (grid) {
+            md.density = grid->data().data();
+            if ((rc = xrt_set_medium(m_ctx, &md)) != XRT_OK) return fail(rc, "xrt_set_medium");
+        } else {   // leaf bricks (NanoVDB layout)
+            const xrt_brick_grid bg{sparse->bricksX(), sparse->bricksY(), sparse->bricksZ(), sparse->table().data(),
+                                    sparse->brickCount(), sparse->bricks().data()};
+            if ((rc = xrt_set_medium_bricks(m_ctx, &md, &bg)) != XRT_OK) return fail(rc, "xrt_set_medium_bricks");
+        }
     }
     p.max_depth = integrator->maxDepth();
     p.width = image.getWidth();

@@ -115,6 +115,51 @@ AABB DenseGrid::getBounds() const {
     return b;
 }
 
+SparseGrid::SparseGrid(uint32_t nx, uint32_t ny, uint32_t nz, std::vector<int32_t> table, std::vector<float> bricks,
+                       Vec3f origin, float voxelSize)
+    : nx_(nx), ny_(ny), nz_(nz), table_(std::move(table)), bricks_(std::move(bricks)), origin_(origin), voxel_(voxelSize) {}
+
+SparseGrid SparseGrid::fromDense(uint32_t nx, uint32_t ny, uint32_t nz, const std::vector<float>& d, Vec3f origin,
+                                 float voxelSize) {
+    const uint32_t B = kBrick, bx = (nx + B - 1) / B, by = (ny + B - 1) / B, bz = (nz + B - 1) / B;
+    std::vector<int32_t> table((size_t)bx * by * bz, -1);
+    std::vector<float> bricks;
+    std::vector<float> leaf(B * B * B);
+    for (uint32_t k = 0; k < bz; ++k)
+        for (uint32_t j = 0; j < by; ++j)
+            for (uint32_t i = 0; i < bx; ++i) {
+                bool any = false;
+                for (uint32_t z = 0; z < B; ++z)
+                    for (uint32_t y = 0; y < B; ++y)
+                        for (uint32_t x = 0; x < B; ++x) {
+                            const uint32_t gx = i * B + x, gy = j * B + y, gz = k * B + z;
+                            const float v = gx < nx && gy < ny && gz < nz ? d[((size_t)gz * ny + gy) * nx + gx] : 0.0f;
+                            leaf[(z * B + y) * B + x] = v;
+                            any |= v != 0.0f;
+                        }
+                if (!any) continue;
+                table[((size_t)k * by + j) * bx + i] = (int32_t)(bricks.size() / leaf.size());
+                bricks.insert(bricks.end(), leaf.begin(), leaf.end());
+            }
+    return SparseGrid(nx, ny, nz, std::move(table), std::move(bricks), origin, voxelSize);
+}
+
+AABB SparseGrid::getBounds() const {   // as DenseGrid::getBounds
+    AABB b;
+    const double n[3] = {(double)nx_ - 1.0, (double)ny_ - 1.0, (double)nz_ - 1.0};
+    for (int i = 0; i < 3; ++i) {
+        b.pMin[i] = (float)(0.0 * (double)voxel_ + (double)origin_[i]);
+        b.pMax[i] = (float)(n[i] * (double)voxel_ + (double)origin_[i]);
+    }
+    return b;
+}
+
+float SparseGrid::getMaxDensity() const {   // inactive voxels read 0
+    float m = 0.0f;
+    for (float v : bricks_) m = std::max(m, v);
+    return m;
+}
+
 float DenseGrid::getMaxDensity() const {  // evalMinMax (Src/grid.h:79-83)
     float m = data_.empty() ? 0.0f : data_[0];
     for (float v : data_) m = std::max(m, v);

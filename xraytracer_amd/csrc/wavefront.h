@@ -121,6 +121,11 @@ struct DMedium {
     int kind;              // XRT_MEDIUM_* (0 heterogeneous: delta / ratio tracking)
     float sigma_t[3];      // homogeneous kinds: sigma_a + sigma_s (HomogeneousMedium ctor)
     double inv_voxel;      // 1.0 / (double)voxel_size, once on the host (same IEEE quotient)
+    // sparse leaf bricks (xrt_set_medium_bricks): table[(bz*nby + by)*nbx + bx] -> brick or -1;
+    // null for the dense grid
+    const int* brick_table;
+    const float* bricks;
+    int nbx, nby, nbz;
 };
 
 #ifdef __HIPCC__

@@ -428,6 +428,12 @@ __device__ __forceinline__ float grid_value(const DMedium& M, int i, int j, int 
     return M.density[((size_t)k * M.ny + (size_t)j) * M.nx + (size_t)i];
 }
 __device__ __forceinline__ float vdb_lerp(float a, float b, double w) { return a + (float)((double)(b - a) * w); }
+// sparse leaf bricks: one voxel (background 0 outside the grid and in inactive bricks)
+__device__ __forceinline__ float brick_value(const DMedium& M, int i, int j, int k) {
+    if (i < 0 || j < 0 || k < 0 || i >= M.nx || j >= M.ny || k >= M.nz) return 0.0f;
+    const int b = M.brick_table[((k >> 3) * M.nby + (j >> 3)) * M.nbx + (i >> 3)];
+    return b < 0 ? 0.0f : M.bricks[(size_t)b * 512 + (((k & 7) * 8 + (j & 7)) * 8 + (i & 7))];
+}
 __device__ float medium_density(const DMedium& M, v3 p) {
     const double inv = M.inv_voxel;
     const double xi = ((double)p.x - (double)M.origin[0]) * inv;
@@ -437,7 +443,25 @@ __device__ float medium_density(const DMedium& M, v3 p) {
     const int i = (int)fx, j = (int)fy, k = (int)fz;
     const double u = xi - fx, v = yi - fy, w = zi - fz;
     float d000, d001, d010, d011, d100, d101, d110, d111;
-    if (i >= 0 && j >= 0 && k >= 0 && i + 1 < M.nx && j + 1 < M.ny && k + 1 < M.nz) {
+    if (M.brick_table) {
+        // a cell inside one brick: one table lookup, x-neighbours adjacent in the brick
+        if (i >= 0 && j >= 0 && k >= 0 && i + 1 < M.nx && j + 1 < M.ny && k + 1 < M.nz && (i & 7) != 7 &&
+            (j & 7) != 7 && (k & 7) != 7) {
+            const int b = M.brick_table[((k >> 3) * M.nby + (j >> 3)) * M.nbx + (i >> 3)];
+            if (b < 0) {
+                d000 = d001 = d010 = d011 = d100 = d101 = d110 = d111 = 0.0f;
+            } else {
+                const float* q = M.bricks + (size_t)b * 512 + (((k & 7) * 8 + (j & 7)) * 8 + (i & 7));
+                d000 = q[0], d100 = q[1], d010 = q[8], d110 = q[9];
+                d001 = q[64], d101 = q[65], d011 = q[72], d111 = q[73];
+            }
+        } else {
+            d000 = brick_value(M, i, j, k), d001 = brick_value(M, i, j, k + 1);
+            d010 = brick_value(M, i, j + 1, k), d011 = brick_value(M, i, j + 1, k + 1);
+            d100 = brick_value(M, i + 1, j, k), d101 = brick_value(M, i + 1, j, k + 1);
+            d110 = brick_value(M, i + 1, j + 1, k), d111 = brick_value(M, i + 1, j + 1, k + 1);
+        }
+    } else if (i >= 0 && j >= 0 && k >= 0 && i + 1 < M.nx && j + 1 < M.ny && k + 1 < M.nz) {
         // interior cell: the x-neighbours are adjacent words, four dword-aligned dwordx2 loads
         typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
         using g2 = __attribute__((address_space(1))) const f2u;

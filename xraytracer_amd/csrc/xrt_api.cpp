@@ -61,6 +61,7 @@ struct xrt_ctx {
     // a mesh), and the query's own buffers
     std::vector<int> obj_tri_first;
     DevBuf q_rays, q_tmax, q_out;
+    DevBuf brick_table, brick_data;   // sparse medium (xrt_set_medium_bricks)
     DevBuf stage;              // multi: device-output staging on subs[0] (accumulate from a device image)
 };
 
@@ -157,6 +158,7 @@ void xrt_destroy(xrt_ctx* c) {
                      &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch, &c->kparams};
     for (DevBuf* b : all) free_buf(*b);
     free_buf(c->stage), free_buf(c->q_rays), free_buf(c->q_tmax), free_buf(c->q_out);
+    free_buf(c->brick_table), free_buf(c->brick_data);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->poll_ev)
         if (e) (void)hipEventDestroy(e);
@@ -399,6 +401,8 @@ static int set_camera_one(xrt_ctx* c, const float c2w[16], float scale, float as
     return XRT_OK;
 }
 
+static int set_medium_grid(xrt_ctx* c, const xrt_medium_desc* m);
+
 static int set_medium_one(xrt_ctx* c, const xrt_medium_desc* m) {
     if (!c || !m) return XRT_ERR_INVALID;
     if (m->kind != XRT_MEDIUM_HETEROGENEOUS) {
@@ -421,7 +425,14 @@ static int set_medium_one(xrt_ctx* c, const xrt_medium_desc* m) {
     int rc = upload(c, c->density, m->density, n * sizeof(float));
     if (rc) return rc;
     DMedium& D = c->base.medium;
+    D = DMedium{};
     D.density = as<float>(c->density);
+    return set_medium_grid(c, m);
+}
+
+// the grid-independent part of a heterogeneous medium (dense or bricks)
+static int set_medium_grid(xrt_ctx* c, const xrt_medium_desc* m) {
+    DMedium& D = c->base.medium;
     D.nx = (int)m->nx, D.ny = (int)m->ny, D.nz = (int)m->nz;
     for (int q = 0; q < 3; ++q) {
         D.origin[q] = m->origin[q];
@@ -441,6 +452,41 @@ static int set_medium_one(xrt_ctx* c, const xrt_medium_desc* m) {
     D.majorant = std::max(mm[0], std::max(mm[1], mm[2]));
     D.inv_majorant = 1.0f / D.majorant;
     c->has_medium = true;
+    return XRT_OK;
+}
+
+// Sparse heterogeneous density in XRT_BRICK^3 leaf bricks (the NanoVDB / OpenVDB leaf
+// layout): the same trilinear BoxSampler as the dense grid, reading voxels through the brick
+// table (medium_density), so inactive regions cost no memory.
+static int set_medium_bricks_one(xrt_ctx* c, const xrt_medium_desc* m, const xrt_brick_grid* g) {
+    if (!c || !m || !g) return XRT_ERR_INVALID;
+    if (m->kind != XRT_MEDIUM_HETEROGENEOUS) return set_err(c, XRT_ERR_INVALID, "brick grids are heterogeneous media");
+    if (!m->nx || !m->ny || !m->nz || !g->table || (g->n_bricks && !g->bricks) || g->nbx != (m->nx + 7) / 8 ||
+        g->nby != (m->ny + 7) / 8 || g->nbz != (m->nz + 7) / 8)
+        return set_err(c, XRT_ERR_INVALID, "brick table dimensions do not match the grid (ceil(n / 8) per axis)");
+    const size_t nt = (size_t)g->nbx * g->nby * g->nbz;
+    for (size_t i = 0; i < nt; ++i)
+        if (g->table[i] < -1 || g->table[i] >= (int32_t)g->n_bricks)
+            return set_err(c, XRT_ERR_INVALID, "brick table entry out of range");
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = upload(c, c->brick_table, g->table, nt * sizeof(int32_t))) ||
+        (rc = upload(c, c->brick_data, g->bricks, (size_t)g->n_bricks * 512 * sizeof(float))))
+        return rc;
+    DMedium& D = c->base.medium;
+    D = DMedium{};
+    D.brick_table = as<int>(c->brick_table);
+    D.bricks = as<float>(c->brick_data);
+    D.nbx = (int)g->nbx, D.nby = (int)g->nby, D.nbz = (int)g->nbz;
+    return set_medium_grid(c, m);
+}
+
+int xrt_set_medium_bricks(xrt_ctx* c, const xrt_medium_desc* m, const xrt_brick_grid* g) {
+    if (!c || c->subs.empty()) return set_medium_bricks_one(c, m, g);
+    for (xrt_ctx* d : c->subs) {
+        const int rc = set_medium_bricks_one(d, m, g);
+        if (rc) return set_err(c, rc, "xrt_set_medium_bricks on device " + std::to_string(d->device) + ": " + d->err);
+    }
     return XRT_OK;
 }
 

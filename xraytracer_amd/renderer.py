@@ -54,7 +54,16 @@ class HipRenderer:
                                              C.c_float(cam.aspect)), "xrt_set_camera")
         if scene.medium is not None:
             md = scene.medium.desc()
-            self._check(self._lib.xrt_set_medium(self.ctx, C.byref(md)), "xrt_set_medium")
+            if getattr(scene.medium, "sparse", False):
+                table, bricks = scene.medium.bricks()
+                self._bricks = (table, bricks)   # alive until the library has copied them
+                nbz, nby, nbx = table.shape
+                bg = abi.XrtBrickGrid(nbx, nby, nbz, table.ctypes.data_as(C.POINTER(C.c_int32)), len(bricks),
+                                      abi.fptr(bricks.reshape(-1)))
+                self._check(self._lib.xrt_set_medium_bricks(self.ctx, C.byref(md), C.byref(bg)),
+                            "xrt_set_medium_bricks")
+            else:
+                self._check(self._lib.xrt_set_medium(self.ctx, C.byref(md)), "xrt_set_medium")
         self._uploaded = scene
 
     def params(self, scene, width, height, shard_index=0, shard_count=1, timing=False, integrator=None,

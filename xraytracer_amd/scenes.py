@@ -52,6 +52,21 @@ class Medium:
     absorption: tuple
     scattering: tuple
     multiplier: float = 1.0
+    sparse: bool = False     # upload as 8^3 leaf bricks (xrt_set_medium_bricks), same image
+
+    def bricks(self):
+        """(table [nbz, nby, nbx] int32 brick index or -1, bricks [n, 8, 8, 8] float32): the
+        grid cut into XRT_BRICK^3 leaves, all-zero leaves dropped (SparseGrid::fromDense)."""
+        B = abi.XRT_BRICK
+        nz, ny, nx = self.density.shape
+        nb = [(n + B - 1) // B for n in (nz, ny, nx)]
+        pad = np.zeros([n * B for n in nb], np.float32)
+        pad[:nz, :ny, :nx] = self.density
+        leaves = pad.reshape(nb[0], B, nb[1], B, nb[2], B).transpose(0, 2, 4, 1, 3, 5).reshape(-1, B, B, B)
+        keep = np.any(leaves != 0.0, axis=(1, 2, 3))
+        table = np.full(len(leaves), -1, np.int32)
+        table[keep] = np.arange(int(keep.sum()), dtype=np.int32)
+        return table.reshape(nb), np.ascontiguousarray(leaves[keep])
 
     def bounds(self):
         nz, ny, nx = self.density.shape
