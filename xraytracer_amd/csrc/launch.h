@@ -41,7 +41,7 @@ uint32_t step_merged_draws(const KParams& P);
 uint32_t step_merged_spw(const KParams& P, uint64_t live);   // slots per wave for `live` live slots
 uint32_t step_merged_group(const KParams& P, uint32_t spw);  // lanes per slot in group traces (1 = none)
 size_t step_merged_lds_bytes(const KParams& P);
-void build_step_objs(const DObjBox* boxes, int n, StepObjs& SO);
+void build_step_objs(const DObjBox* boxes, const DObjPlane* planes, int n, StepObjs& SO);
 hipError_t launch_step_merged(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                               const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
                               uint32_t* req_count, uint32_t visits, uint64_t live, hipStream_t st);

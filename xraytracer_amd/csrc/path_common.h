@@ -379,9 +379,24 @@ __device__ __forceinline__ v3 eval_bxdf(const DObj& ob) {   // Lambert::evaluate
     return ob.material == 1 ? ld3(ob.fr) : mk(0, 0, 0);   // albedo / PI, divided on the host
 }
 
+// x / (float)width, x / (float)height, x / aspect — the renderer's constant divisors.  Where
+// the host proved Markstein's correction with its RN(1/c) equal to IEEE division for every
+// mantissa of x (KParams::cdiv, xrt_api.cpp cdiv_exact), div_const's three operations
+// replace the IEEE sequence; otherwise the IEEE division.  The flag is uniform: no
+// divergence.
+__device__ __forceinline__ float div_w(const KParams& P, float x) {
+    return (P.cdiv & 1u) ? div_const(x, P.fw, P.rw) : x / (float)P.width;
+}
+__device__ __forceinline__ float div_h(const KParams& P, float x) {
+    return (P.cdiv & 2u) ? div_const(x, P.fh, P.rh) : x / (float)P.height;
+}
+__device__ __forceinline__ float div_a(const KParams& P, float x) {
+    return (P.cdiv & 4u) ? div_const(x, P.aspect, P.raspect) : x / P.aspect;
+}
+
 // PinholeCamera::sampleRay (Src/camera.h:49-60)
 __device__ __forceinline__ void camera_ray(const KParams& P, float u, float v, v3& o, v3& d) {
-    const v3 dir = mk((2.0f * u - 1.0f) * P.scale, (1.0f - 2.0f * v) * P.scale / P.aspect, -1.0f);
+    const v3 dir = mk((2.0f * u - 1.0f) * P.scale, div_a(P, (1.0f - 2.0f * v) * P.scale), -1.0f);
     const float* x = P.c2w;
     const v3 w = mk(dir.x * x[0] + dir.y * x[4] + dir.z * x[8], dir.x * x[1] + dir.y * x[5] + dir.z * x[9],
                     dir.x * x[2] + dir.y * x[6] + dir.z * x[10]);

@@ -112,6 +112,13 @@ struct RngRegs {
     }
 };
 
+// LDS of k_step_merged: the scene (step_layout), the per-object planes (group traces), then
+// one MergedWave of trace scratch per wave
+__host__ __device__ inline uint32_t merged_plane_off(const StepLayout& Lo) { return (Lo.total + 15u) & ~15u; }
+__host__ __device__ inline uint32_t merged_wave_off(const KParams& P, const StepLayout& Lo) {
+    return merged_plane_off(Lo) + ((8u * (uint32_t)P.n_objs + 15u) & ~15u);
+}
+
 template <int NL>
 struct MergedWave {
     static constexpr int R = 1 + NL;   // rays per lane: extension + one shadow ray per light
@@ -122,18 +129,52 @@ struct MergedWave {
     uint32_t list[R * 64];             // ranked rays (q * 64 + lane) of the current object
 };
 
+// A float that is +0, -0 or NaN as a 2-bit code (0, 1, 2) and back (NaN: the canonical
+// quiet NaN — a NaN contribution makes its sample's radiance NaN, which Image::addPixel's
+// reject drops, so the payload never reaches the image)
+__device__ __forceinline__ uint32_t zcode(float x) { return x != x ? 2u : (__float_as_uint(x) >> 31); }
+__device__ __forceinline__ float zdecode(uint32_t c) {
+    return __uint_as_float(c == 2u ? 0x7fc00000u : (c << 31));
+}
+
 __device__ __forceinline__ uint32_t lanemask_rank(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Conservative overlap of the ray segment [0, tlim] with the object's culling box.
-__device__ __forceinline__ bool obj_overlap(v3 o, v3 inv, const StepObj& B, float tlim) {
-    const float tx0 = (B.bmin[0] - o.x) * inv.x, tx1 = (B.bmax[0] - o.x) * inv.x;
-    const float ty0 = (B.bmin[1] - o.y) * inv.y, ty1 = (B.bmax[1] - o.y) * inv.y;
-    const float tz0 = (B.bmin[2] - o.z) * inv.z, tz1 = (B.bmax[2] - o.z) * inv.z;
+// Conservative overlap of the ray segment [0, tlim] with the object's culling box.  oi = o *
+// inv, once per ray: each slab distance is one fma, b * inv - oi, whose error (~2^-24 |o|
+// along the axis) is far inside the box margin; NaNs (0 * inf for axis-parallel rays) are
+// dropped by fminf / fmaxf, which only widens the interval.
+__device__ __forceinline__ bool obj_overlap(v3 oi, v3 inv, const StepObj& B, float tlim) {
+    const float tx0 = __builtin_fmaf(B.bmin[0], inv.x, -oi.x), tx1 = __builtin_fmaf(B.bmax[0], inv.x, -oi.x);
+    const float ty0 = __builtin_fmaf(B.bmin[1], inv.y, -oi.y), ty1 = __builtin_fmaf(B.bmax[1], inv.y, -oi.y);
+    const float tz0 = __builtin_fmaf(B.bmin[2], inv.z, -oi.z), tz1 = __builtin_fmaf(B.bmax[2], inv.z, -oi.z);
     const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
     const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
     return !(tn > tf);
+}
+__device__ __forceinline__ bool box_overlap_f(v3 oi, v3 inv, const DObjBox& B, float tlim) {
+    const float tx0 = __builtin_fmaf(B.bmin[0], inv.x, -oi.x), tx1 = __builtin_fmaf(B.bmax[0], inv.x, -oi.x);
+    const float ty0 = __builtin_fmaf(B.bmin[1], inv.y, -oi.y), ty1 = __builtin_fmaf(B.bmax[1], inv.y, -oi.y);
+    const float tz0 = __builtin_fmaf(B.bmin[2], inv.z, -oi.z), tz1 = __builtin_fmaf(B.bmax[2], inv.z, -oi.z);
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
+    return !(tn > tf);
+}
+
+// Exact plane cull.  Every vertex of the object has coordinate c on axis a (DObjPlane), so
+// e1_a = e2_a = 0 exactly and, in Mesh::rayTriangleIntersect's float evaluation, every term
+// of det = e1 . (d x e2) and of t's numerator e2 . ((o - v0) x e1) that involves e1_a or e2_a
+// is an exact +-0: det is d_a (A - B) and the numerator -(o_a - c) (A - B), up to roundings
+// that cannot flip the sign of A - B (plane_tri_ok, host).  So whenever (o_a - c) * d_a >= 0
+// the test rejects every triangle of the object: t = num / det <= 0, or d_a = 0 gives
+// |det| < eps, or o_a = c gives t = +-0.  (Where |d_a| < 1e-20 or |o_a - c| < 1e-25 a
+// product may leave the normal range, but then |det| < eps resp. |t| < eps for the edge
+// lengths plane_tri_ok admits, so the test rejects anyway.)  NaNs are not culled.
+__device__ __forceinline__ bool plane_away(v3 o, v3 d, int axis, float c) {
+    const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+    const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+    return axis >= 0 && (oa - c) * da >= 0.0f;
 }
 
 // Mesh::rayTriangleIntersect (Src/primitive.cpp:140-168) without branches: the same float
@@ -167,19 +208,21 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
     W.occ[lane] = 0u;
     W.ro[lane] = make_float4(o.x, o.y, o.z, kINF);
     W.rd[lane] = make_float4(d.x, d.y, d.z, 0.0f);
-    v3 inv[R];
+    v3 inv[R], oi[R];
     inv[0] = rcp3(d);
+    oi[0] = o * inv[0];
 #pragma unroll
-    for (int l = 0; l < NL; ++l) inv[1 + l] = rcp3(sd[l]);
+    for (int l = 0; l < NL; ++l) inv[1 + l] = rcp3(sd[l]), oi[1 + l] = so[l] * inv[1 + l];
     wave_sync();
     const int n = SO.n;
     for (int ob = 0; ob < n; ++ob) {
         const StepObj B = SO.o[ob];
         bool need[R];
-        need[0] = ext && obj_overlap(o, inv[0], B, kINF);
+        need[0] = ext && !plane_away(o, d, B.axis, B.plane) && obj_overlap(oi[0], inv[0], B, kINF);
 #pragma unroll
         for (int l = 0; l < NL; ++l)
-            need[1 + l] = B.occluder && ((shm >> l) & 1u) && obj_overlap(so[l], inv[1 + l], B, stm[l]);
+            need[1 + l] = B.occluder && ((shm >> l) & 1u) && !plane_away(so[l], sd[l], B.axis, B.plane) &&
+                          obj_overlap(oi[1 + l], inv[1 + l], B, stm[l]);
         uint32_t tot = 0;
 #pragma unroll
         for (int q = 0; q < R; ++q) {
@@ -253,28 +296,32 @@ __device__ __forceinline__ uint64_t group_min64(uint64_t x) {
 }
 
 template <int NL, int G>
-__device__ __forceinline__ void group_trace(int n_objs, const LScene& L, int lane, bool ext, v3 o, v3 d,
+__device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const DObjPlane* pl, int lane, bool ext, v3 o, v3 d,
                                             uint32_t shm, const v3 (&so)[NL + 1], const v3 (&sd)[NL + 1],
                                             const float (&stm)[NL + 1], unsigned long long& best, uint32_t& occ) {
     constexpr int R = 1 + NL;
     const int u = lane & (G - 1);
     uint64_t tm[R];
-    v3 inv[R];
+    v3 inv[R], oi[R];
 #pragma unroll
     for (int q = 0; q < R; ++q) tm[q] = 0ull;
     inv[0] = rcp3(d);
+    oi[0] = o * inv[0];
 #pragma unroll
-    for (int l = 0; l < NL; ++l) inv[1 + l] = rcp3(sd[l]);
+    for (int l = 0; l < NL; ++l) inv[1 + l] = rcp3(sd[l]), oi[1 + l] = so[l] * inv[1 + l];
     for (int ob0 = 0; ob0 < n_objs; ob0 += G) {
         const int ob = ob0 + u;
         if (ob < n_objs) {
             const DObjBox B = L.box[ob];
+            const DObjPlane pb = pl[ob];
             const uint32_t cnt = (uint32_t)(B.count_occ & 0x7fffffff);
             const uint64_t bits = (cnt >= 64u ? ~0ull : ((1ull << cnt) - 1ull)) << B.first;
-            if (ext && box_overlap(o, inv[0], B, kINF)) tm[0] |= bits;
+            if (ext && !plane_away(o, d, pb.axis, pb.c) && box_overlap_f(oi[0], inv[0], B, kINF)) tm[0] |= bits;
 #pragma unroll
             for (int l = 0; l < NL; ++l)
-                if (B.count_occ < 0 && ((shm >> l) & 1u) && box_overlap(so[l], inv[1 + l], B, stm[l])) tm[1 + l] |= bits;
+                if (B.count_occ < 0 && ((shm >> l) & 1u) && !plane_away(so[l], sd[l], pb.axis, pb.c) &&
+                    box_overlap_f(oi[1 + l], inv[1 + l], B, stm[l]))
+                    tm[1 + l] |= bits;
         }
     }
     const uint64_t pat = (G == 4 ? 0x1111111111111111ull : G == 2 ? 0x5555555555555555ull : ~0ull) << u;
@@ -463,14 +510,18 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
     L.light = reinterpret_cast<const DLight*>(lb + Lo.light);
     L.sobj = reinterpret_cast<const int*>(lb + Lo.sobj);
     const int tid = threadIdx.x, lane = tid & 63;
-    MergedWave<NL>& W = reinterpret_cast<MergedWave<NL>*>(lb + ((Lo.total + 15u) & ~15u))[tid >> 6];
+    const DObjPlane* lplane = reinterpret_cast<const DObjPlane*>(lb + merged_plane_off(Lo));
+    MergedWave<NL>& W = reinterpret_cast<MergedWave<NL>*>(lb + merged_wave_off(P, Lo))[tid >> 6];
     static_assert(sizeof(MergedWave<NL>) >= kMT * 4, "the wave's trace scratch doubles as the refill buffer");
     lds_copy(const_cast<f4*>(L.tri), P.tri, 3 * P.n_tris, tid);
     lds_copy(const_cast<f4*>(L.tng), P.tri_ng, P.n_tris, tid);
     lds_copy(const_cast<f4*>(L.nrm), P.tri_nrm, 3 * P.n_tris, tid);
     lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
     lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid);
-    if (LANE) lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid);
+    if (LANE) {
+        lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid);
+        lds_copy(const_cast<DObjPlane*>(lplane), P.obj_plane, P.n_objs, tid);
+    }
     __syncthreads();
 #ifdef XRT_PHASE_CLOCK
     uint64_t ph_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -495,6 +546,12 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
         v3 thr = mk(1, 1, 1), rad = mk(0, 0, 0), o = mk(0, 0, 0), d = mk(0, 0, 0), acc = mk(0, 0, 0);
         v3 rad_fin = mk(0, 0, 0), thr_nee = mk(0, 0, 0);
         v3 so[NL + 1], sd[NL + 1], c1[NL + 1], c0[NL + 1];
+        // GI with one light: the NEE term is folded at sampling time — c1[0] holds
+        // thr * (0 + (0 + c1)) and c0z the codes of thr * (0 + (0 + c0)) (each component +-0 or
+        // NaN), the exact values resolve() would form from thr_nee and c0 / c1 — so neither
+        // thr_nee nor c0 stays live across the trace
+        constexpr bool kFold = INTEG == XRT_INTEGRATOR_GI && NL == 1;
+        uint32_t c0z = 0;
         float stm[NL + 1];
 #pragma unroll
         for (int l = 0; l <= NL; ++l) so[l] = sd[l] = c1[l] = c0[l] = mk(0, 0, 0), stm[l] = 0.0f;
@@ -533,8 +590,8 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
         };
         // jitter draws + PinholeCamera::sampleRay for the next sample (Src/renderer.cpp:44-50)
         auto start_sample = [&]() {
-            const float u = ((float)(int)col + rng.next()) / (float)width;
-            const float v = ((float)(int)row + rng.next()) / (float)height;
+            const float u = div_w(P, (float)(int)col + rng.next());
+            const float v = div_h(P, (float)(int)row + rng.next());
             camera_ray(P, u, v, o, d);
             thr = mk(1, 1, 1), rad = mk(0, 0, 0);
             depth = 0;
@@ -550,6 +607,8 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
 #pragma unroll
                 for (int l = 0; l < NL; ++l)
                     if ((shm >> l) & 1u) tgt = tgt + (((occ >> l) & 1u) ? c0[l] : c1[l]);
+            } else if constexpr (kFold) {
+                tgt = tgt + ((occ & 1u) ? mk(zdecode(c0z & 3u), zdecode((c0z >> 2) & 3u), zdecode(c0z >> 4)) : c1[0]);
             } else {
                 v3 directL = mk(0, 0, 0);
 #pragma unroll
@@ -585,7 +644,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
             if constexpr (!LANE)
                 merged_trace<NL>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ PH_TARGS);
             else
-                group_trace<NL, G>(P.n_objs, L, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
+                group_trace<NL, G>(P.n_objs, L, lplane, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
             MPH_MARK(1);
             resolve(occ);
             if (vis > 0) rng.take();   // the words prefetched at the end of the previous segment
@@ -661,13 +720,19 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                             c1[l] = ((fr * Lv) * cosv) / pdf;
                             const v3 z = ((fr * 0.0f) * Lv) * cosv;
                             c0[l] = pdf == pdf ? z : mk(pdf, pdf, pdf);
+                            if constexpr (kFold) {   // GIIntegrator: rad += thr * directL (resolve)
+                                const v3 zero = mk(0, 0, 0);
+                                c1[0] = thr * (zero + (zero + c1[0]));
+                                const v3 w = thr * (zero + (zero + c0[0]));
+                                c0z = zcode(w.x) | (zcode(w.y) << 2) | (zcode(w.z) << 4);
+                            }
                         }
                     }
                     MPH_MARK(10);
                     if (INTEG == XRT_INTEGRATOR_DIRECT) {
                         ended = true;
                     } else {
-                        if (shm) thr_nee = thr;
+                        if (!kFold && shm) thr_nee = thr;
                         else rad = rad + thr * mk(0.0f, 0.0f, 0.0f);   // no shadow ray: directL = 0
                         v3 nd = mk(0, 0, 0);
                         const bool lamb = ob.material == 1;
@@ -715,7 +780,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
             if constexpr (!LANE)
                 merged_trace<NL>(SO, L, W, lane, false, o, d, shm, so, sd, stm, best, occ PH_TARGS);
             else
-                group_trace<NL, G>(P.n_objs, L, lane, false, o, d, shm, so, sd, stm, best, occ);
+                group_trace<NL, G>(P.n_objs, L, lplane, lane, false, o, d, shm, so, sd, stm, best, occ);
             resolve(occ);
         }
         MPH_MARK(5);
@@ -824,14 +889,16 @@ size_t step_merged_lds_bytes(const KParams& P) {
         case 3: w = sizeof(MergedWave<3>); break;
         default: w = sizeof(MergedWave<4>); break;
     }
-    return ((step_layout(P).total + 15u) & ~15u) + (kBlock / 64) * w;
+    return merged_wave_off(P, step_layout(P)) + (kBlock / 64) * w;
 }
 
-void build_step_objs(const DObjBox* boxes, int n, StepObjs& SO) {
+void build_step_objs(const DObjBox* boxes, const DObjPlane* planes, int n, StepObjs& SO) {
     std::memset(&SO, 0, sizeof(SO));
     SO.n = n;
     for (int i = 0; i < n; ++i) {
         StepObj& o = SO.o[i];
+        o.axis = planes[i].axis;
+        o.plane = planes[i].c;
         for (int q = 0; q < 3; ++q) o.bmin[q] = boxes[i].bmin[q], o.bmax[q] = boxes[i].bmax[q];
         o.first = boxes[i].first;
         o.count = (uint32_t)(boxes[i].count_occ & 0x7fffffff);

@@ -93,6 +93,17 @@ struct StepObj {
     uint32_t count;
     uint32_t magic;
     uint32_t occluder;
+    int axis;      // DObjPlane of the object
+    float plane;
+};
+// Axis-aligned plane of a mesh object whose every vertex has the same coordinate `c` on
+// axis `axis` (-1: no such plane).  Every Moller-Trumbore test of such an object by a ray
+// whose origin lies on one side of the plane and whose direction does not point back at it
+// returns t <= 0 (or |det| < eps), so the merged-trace kernels skip the object for that ray
+// without a box test (plane_away, step_tri.hip; the argument is in DESIGN.md §3).
+struct DObjPlane {
+    int axis;
+    float c;
 };
 constexpr int kMergedMaxObjs = 32;
 struct StepObjs {
@@ -146,6 +157,7 @@ struct KParams {
     const DLight* lights;
     const DSeg* segs;
     const DObjBox* obj_box;   // per object, for the small-scene trace path (n_objs entries)
+    const DObjPlane* obj_plane;   // per object, small triangle scenes (n_objs entries)
     const f4* bvh_node;       // large triangle scenes: BvhNode array (4 f4 each, bvh.h), else null
     const f4* bvh_tri;        // triangles in BVH leaf order, as `tri` but e2.w = original index
     int bvh_stack;            // k_trace_bvh: LDS stack entries per thread (tree depth + 1 <= kBvhStack)
@@ -159,6 +171,9 @@ struct KParams {
     // ---- camera (row-major c2w) + PinholeCamera scale / aspect
     float c2w[16];
     float scale, aspect;
+    float raspect;               // RN(1 / aspect)
+    float fw, fh, rw, rh;        // (float)width, (float)height and their RN reciprocals
+    uint32_t cdiv;               // bit 0/1/2: x / width, height, aspect may use div_const (host-proven)
     // ---- render
     int integrator;
     uint32_t max_depth, width, height, spp, shard_index, shard_count, n_slots;

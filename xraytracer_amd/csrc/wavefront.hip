@@ -957,8 +957,8 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
                 }
                 // regenerate: jitter draws, camera ray
                 const uint32_t col = s % P.width, row = P.shard_index + P.shard_count * (s / P.width);
-                const float u = ((float)(int)col + rng.next()) / (float)P.width;
-                const float v = ((float)(int)row + rng.next()) / (float)P.height;
+                const float u = div_w(P, (float)(int)col + rng.next());
+                const float v = div_h(P, (float)(int)row + rng.next());
                 camera_ray(P, u, v, o, d);
                 thr = mk(1, 1, 1);
                 rad = mk(0, 0, 0);
@@ -974,8 +974,8 @@ __global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __r
             if (st & ST_REGEN) {   // very first sample of the slot
                 st &= ~ST_REGEN;
                 const uint32_t col = s % P.width, row = P.shard_index + P.shard_count * (s / P.width);
-                const float u = ((float)(int)col + rng.next()) / (float)P.width;
-                const float v = ((float)(int)row + rng.next()) / (float)P.height;
+                const float u = div_w(P, (float)(int)col + rng.next());
+                const float v = div_h(P, (float)(int)row + rng.next());
                 camera_ray(P, u, v, o, d);
                 thr = mk(1, 1, 1);
                 rad = mk(0, 0, 0);
@@ -1391,8 +1391,8 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
             if (st & ST_REGEN) {
                 // next sample: jitter draws + camera ray (Src/renderer.cpp:44-50)
                 st &= ~ST_REGEN;
-                const float u = ((float)(int)col + rng.next()) / (float)P.width;
-                const float v = ((float)(int)row + rng.next()) / (float)P.height;
+                const float u = div_w(P, (float)(int)col + rng.next());
+                const float v = div_h(P, (float)(int)row + rng.next());
                 camera_ray(P, u, v, o, d);
                 thr = mk(1, 1, 1), rad = mk(0, 0, 0);
                 depth = 0;
@@ -1577,8 +1577,8 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, cons
                     rad = mk(0, 0, 0);
                     ended = true;
                 } else {
-                    const float u = ((float)(int)col + rng.next()) / (float)P.width;
-                    const float v = ((float)(int)row + rng.next()) / (float)P.height;
+                    const float u = div_w(P, (float)(int)col + rng.next());
+                    const float v = div_h(P, (float)(int)row + rng.next());
                     camera_ray(P, u, v, o, d);
                     thr = mk(1, 1, 1), rad = mk(0, 0, 0);
                     depth = 0;
@@ -1815,8 +1815,8 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
             if (act && (st & ST_REGEN)) {
                 // first sample of the slot: jitter draws + camera ray (Src/renderer.cpp:44-50)
                 st &= ~ST_REGEN;
-                const float u = ((float)(int)col + rng.next()) / (float)P.width;
-                const float v = ((float)(int)row + rng.next()) / (float)P.height;
+                const float u = div_w(P, (float)(int)col + rng.next());
+                const float v = div_h(P, (float)(int)row + rng.next());
                 camera_ray(P, u, v, o, d);
                 thr = mk(1, 1, 1), rad = mk(0, 0, 0);
                 depth = 0;
@@ -1941,8 +1941,8 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
                     rad = mk(0, 0, 0);
                     ended = true;
                 } else {
-                    const float u = ((float)(int)col + rng.next()) / (float)P.width;
-                    const float v = ((float)(int)row + rng.next()) / (float)P.height;
+                    const float u = div_w(P, (float)(int)col + rng.next());
+                    const float v = div_h(P, (float)(int)row + rng.next());
                     camera_ray(P, u, v, o, d);
                     thr = mk(1, 1, 1), rad = mk(0, 0, 0);
                     depth = 0;

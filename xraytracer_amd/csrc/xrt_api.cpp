@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <unordered_map>
 #include <cfloat>
 #include <string>
 #include <thread>
@@ -39,8 +40,8 @@ struct xrt_ctx {
     std::string err;
     // scene
     std::vector<DevBuf*> scene_bufs;
-    DevBuf tri, tri_ng, tri_nrm, sph, sph_obj, box, objs, lights, segs, density, obj_box, bvh_node, bvh_tri, snode,
-        ssph, sbk;
+    DevBuf tri, tri_ng, tri_nrm, sph, sph_obj, box, objs, lights, segs, density, obj_box, obj_plane, bvh_node,
+        bvh_tri, snode, ssph, sbk;
     KParams base{};
     StepObjs step_objs{};   // kernel-argument object records of the merged-trace schedule
     bool has_scene = false, has_camera = false, has_medium = false;
@@ -63,6 +64,7 @@ struct xrt_ctx {
     DevBuf q_rays, q_tmax, q_out;
     DevBuf brick_table, brick_data;   // sparse medium (xrt_set_medium_bricks)
     DevBuf stage;              // multi: device-output staging on subs[0] (accumulate from a device image)
+    std::unordered_map<uint32_t, bool> cdiv_cache;   // cdiv_exact results by divisor bits
 };
 
 namespace {
@@ -115,6 +117,58 @@ T* as(DevBuf& b) {
 
 uint32_t shard_rows(uint32_t h, uint32_t idx, uint32_t n) { return idx < h ? (h - idx + n - 1) / n : 0; }
 
+// Is the device's div_const(x, c, RN(1/c)) — q = x * rc, q + (x - c q) * rc with two fmas —
+// equal to the IEEE quotient x / c for every x it is used on?  Within div_const's window
+// (x exponent 25..248) the computation scales exactly with x's exponent (a residual small
+// enough to be subnormal is far below ulp(q) / 2 and cannot change the result), so one
+// binade decides it: all 2^23 mantissas of x in [1, 2) are compared with the host's IEEE
+// division (SSE, correctly rounded).  c is limited to [2^-4, 2^20] so the window's quotients
+// stay normal.  About 10 ms per divisor on 8 threads; results are cached per context.
+bool cdiv_exact(xrt_ctx* c, float d) {
+    if (!(d >= 0x1p-4f && d <= 0x1p20f)) return false;
+    uint32_t key;
+    std::memcpy(&key, &d, 4);
+    auto it = c->cdiv_cache.find(key);
+    if (it != c->cdiv_cache.end()) return it->second;
+    const float rc = 1.0f / d;
+    constexpr int kThreads = 8;
+    bool part[kThreads];
+    std::vector<std::thread> th;
+    for (int t = 0; t < kThreads; ++t)
+        th.emplace_back([&, t] {
+            bool ok = true;
+            for (uint32_t m = (uint32_t)t; m < (1u << 23) && ok; m += kThreads) {
+                const uint32_t xb = 0x3f800000u | m;
+                float x;
+                std::memcpy(&x, &xb, 4);
+                const float q = x * rc;
+                ok = std::fma(std::fma(-d, q, x), rc, q) == x / d;
+            }
+            part[t] = ok;
+        });
+    bool ok = true;
+    for (int t = 0; t < kThreads; ++t) th[t].join(), ok &= part[t];
+    c->cdiv_cache[key] = ok;
+    return ok;
+}
+
+// A triangle of an object lying in the plane x_a = c (e1_a = e2_a = 0 exactly) qualifies for
+// the exact plane cull (DObjPlane, plane_away in step_tri.hip) when the
+// Moller-Trumbore det and t numerator keep the sign of their exact values: with p, q the
+// other two axes, both reduce to (d_a resp. o_a - c) * (e1_p e2_q - e1_q e2_p), each product
+// rounded twice and the difference once, so |A - B| must exceed a few ulps of |A| + |B|.
+// Nonzero edge components within [1e-6, 1e5] keep every product in the normal range for
+// |d_a| >= 1e-20 and |o_a - c| >= 1e-25, and below those |det| resp. |t| stays under
+// FLT_EPSILON, so the test rejects without the sign argument.
+bool plane_tri_ok(const float* e1, const float* e2, int a) {
+    if (e1[a] != 0.0f || e2[a] != 0.0f) return false;
+    const int p = (a + 1) % 3, q = (a + 2) % 3;
+    for (float x : {e1[p], e1[q], e2[p], e2[q]})
+        if (x != 0.0f && !(std::fabs(x) >= 1e-6f && std::fabs(x) <= 1e5f)) return false;
+    const double A = (double)e1[p] * e2[q], B = (double)e1[q] * e2[p];
+    return std::fabs(A - B) > 1e-4 * (std::fabs(A) + std::fabs(B));
+}
+
 
 }  // namespace
 
@@ -152,7 +206,7 @@ void xrt_destroy(xrt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->tri, &c->tri_ng, &c->tri_nrm, &c->sph, &c->sph_obj, &c->box, &c->objs, &c->lights,
-                     &c->segs, &c->density, &c->obj_box, &c->bvh_node, &c->bvh_tri, &c->snode, &c->ssph, &c->sbk, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
+                     &c->segs, &c->density, &c->obj_box, &c->obj_plane, &c->bvh_node, &c->bvh_tri, &c->snode, &c->ssph, &c->sbk, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
                      &c->hit2, &c->hit3, &c->sh_o, &c->sh_d, &c->sh_c, &c->med, &c->med2, &c->nee, &c->state,
                      &c->sample_k, &c->depth, &c->occ, &c->rng_c, &c->rng_g, &c->ring, &c->c_seg, &c->c_shadow,
                      &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch, &c->kparams};
@@ -187,6 +241,7 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
     std::vector<DObj> objs;
     std::vector<DSeg> segs;
     std::vector<int> tri_first(s->n_objects, -1);
+    std::vector<DObjPlane> planes(s->n_objects, DObjPlane{-1, 0.0f});
     auto V = [](const float* p) { return Vec3f(p[0], p[1], p[2]); };
     auto F4 = [](const Vec3f& v, float w) { return f4{v[0], v[1], v[2], w}; };
     auto bits = [](int x) { float f; std::memcpy(&f, &x, 4); return f; };
@@ -200,17 +255,24 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
         objs.push_back(d);
         const bool occluder = o.light < 0;  // Scene::occluded skips area-light objects
         int kind = -1, first = 0;
+        uint32_t axes = 0;   // meshes: DObjPlane candidates
         if (o.kind == XRT_OBJ_MESH) {
             if ((uint64_t)o.first + o.count > s->n_tris || (o.count && (!s->tri_v || !s->tri_n)))
                 return set_err(c, XRT_ERR_INVALID, "mesh range out of bounds");
             kind = SEG_TRI;
             first = (int)(tri.size() / 3);
             tri_first[k] = first;
+            axes = o.count > 0 ? 7u : 0u;   // axes on which every vertex so far shares v[0]'s coordinate
+            const float* vfirst = s->tri_v + 9 * (size_t)o.first;
             for (int t = o.first; t < o.first + o.count; ++t) {
                 const float* v = s->tri_v + 9 * (size_t)t;
                 const float* n = s->tri_n + 9 * (size_t)t;
                 const Vec3f v0 = V(v), v1 = V(v + 3), v2 = V(v + 6);
                 const Vec3f e1 = v1 - v0, e2 = v2 - v0;     // Src/primitive.cpp:142-143
+                for (int a = 0; a < 3; ++a)
+                    if (!(v[a] == vfirst[a] && v[3 + a] == vfirst[a] && v[6 + a] == vfirst[a]) ||
+                        !plane_tri_ok(e1.getPtr(), e2.getPtr(), a))
+                        axes &= ~(1u << a);
                 tri.push_back(F4(v0, bits((int)k)));
                 tri.push_back(F4(e1, occluder ? 1.0f : 0.0f));
                 tri.push_back(F4(e2, 0.0f));
@@ -241,6 +303,13 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
             }
         } else {
             return set_err(c, XRT_ERR_INVALID, "unknown object kind");
+        }
+        if (kind == SEG_TRI && o.count > 0) {
+            for (int a = 0; a < 3; ++a)
+                if ((axes >> a) & 1u) {
+                    planes[k] = DObjPlane{a, s->tri_v[9 * (size_t)o.first + a]};
+                    break;
+                }
         }
         if (o.count == 0) continue;
         if (!segs.empty() && segs.back().kind == kind && segs.back().first + segs.back().count == first)
@@ -313,9 +382,13 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
         const float margin = 1e-3f * diag + 1e-3f;
         for (DObjBox& b : boxes)
             for (int q = 0; q < 3; ++q) b.bmin[q] -= margin, b.bmax[q] += margin;
-        if ((rc = upload(c, c->obj_box, boxes.data(), boxes.size() * sizeof(DObjBox)))) return rc;
+        if ((rc = upload(c, c->obj_box, boxes.data(), boxes.size() * sizeof(DObjBox))) ||
+            (rc = upload(c, c->obj_plane, planes.data(), planes.size() * sizeof(DObjPlane))))
+            return rc;
         P.obj_box = as<DObjBox>(c->obj_box);
-        if (boxes.size() <= (size_t)kMergedMaxObjs) build_step_objs(boxes.data(), (int)boxes.size(), c->step_objs);
+        P.obj_plane = as<DObjPlane>(c->obj_plane);
+        if (boxes.size() <= (size_t)kMergedMaxObjs)
+            build_step_objs(boxes.data(), planes.data(), (int)boxes.size(), c->step_objs);
         P.small_tri = 1;
     }
     // large triangle scenes: a BVH for the wavefront trace (C4's 51k-triangle sphere mesh).
@@ -562,6 +635,9 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     KParams P = c->base;
     P.integrator = p->integrator;
     P.max_depth = p->max_depth, P.width = p->width, P.height = p->height, P.spp = p->spp;
+    P.fw = (float)p->width, P.fh = (float)p->height, P.rw = 1.0f / P.fw, P.rh = 1.0f / P.fh;
+    P.raspect = 1.0f / P.aspect;
+    P.cdiv = (cdiv_exact(c, P.fw) ? 1u : 0u) | (cdiv_exact(c, P.fh) ? 2u : 0u) | (cdiv_exact(c, P.aspect) ? 4u : 0u);
     P.shard_index = p->shard_index, P.shard_count = p->shard_count, P.n_slots = (uint32_t)n;
     P.spw_req = p->slots_per_wave, P.rflags = p->flags;
     // live-list partitions: up to kMaxParts (a multiple of the 8 XCDs), >= 2048 slots each
