@@ -20,6 +20,8 @@ hipError_t launch_seed(const KParams& P, uint32_t* list, uint32_t* count, uint32
                        uint32_t* req_count, hipStream_t st);
 // twist the rings of the slots on P.req (count at *count); clears *zero_count
 hipError_t launch_refill(const KParams& P, const uint32_t* count, uint32_t* zero_count, hipStream_t st);
+hipError_t launch_trace_2a_coop(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
+                                uint32_t blocks, hipStream_t st);
 hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
                         uint32_t blocks, hipStream_t st);
 hipError_t launch_shade(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,

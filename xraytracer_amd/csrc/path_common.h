@@ -234,6 +234,29 @@ __device__ __forceinline__ bool box_overlap(v3 o, v3 inv, const DObjBox& B, floa
     const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
     return !(tn > tf);
 }
+// entry distance of the ray segment [0, tlim] into a padded node box, +inf if it misses
+__device__ __forceinline__ float bvh_enter(const f4& mn, const f4& mx, v3 o, v3 inv, float tlim) {
+    const float tx0 = (mn.x - o.x) * inv.x, tx1 = (mx.x - o.x) * inv.x;
+    const float ty0 = (mn.y - o.y) * inv.y, ty1 = (mx.y - o.y) * inv.y;
+    const float tz0 = (mn.z - o.z) * inv.z, tz1 = (mx.z - o.z) * inv.z;
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
+    return tn > tf ? __builtin_inff() : tn;
+}
+
+// does the ray segment [0, tlim] overlap either child box of a BVH node (n0..n3, bvh.h)?
+__device__ __forceinline__ bool root_overlap(const f4& n0, const f4& n1, const f4& n2, const f4& n3, v3 o, v3 inv,
+                                             float tlim) {
+    const bool l = __float_as_int(n1.w) >= 0 && bvh_enter(n0, n1, o, inv, tlim) != __builtin_inff();
+    const bool r = __float_as_int(n3.w) >= 0 && bvh_enter(n2, n3, o, inv, tlim) != __builtin_inff();
+    return l || r;
+}
+
+// rcp3 clamped to +-1e30 (the fma-form culling slabs, step_tri.hip obj_overlap)
+__device__ __forceinline__ float rcpc(float x) {
+    return __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(x), -1e30f, 1e30f);
+}
+__device__ __forceinline__ v3 rcp3c(v3 d) { return mk(rcpc(d.x), rcpc(d.y), rcpc(d.z)); }
 __device__ __forceinline__ v3 rcp3(v3 d) {
     return mk(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
 }

@@ -143,8 +143,11 @@ __device__ __forceinline__ uint32_t lanemask_rank(uint64_t m) {
 
 // Conservative overlap of the ray segment [0, tlim] with the object's culling box.  oi = o *
 // inv, once per ray: each slab distance is one fma, b * inv - oi, whose error (~2^-24 |o|
-// along the axis) is far inside the box margin; NaNs (0 * inf for axis-parallel rays) are
-// dropped by fminf / fmaxf, which only widens the interval.
+// along the axis, whatever inv) is far inside the box margin.  inv is rcp3c(d): clamped to
+// +-1e30, so no inf enters (an fma of two infinities would be a NaN, and fminf / fmaxf
+// would then keep the wrong slab end); an axis-parallel ray then gets slab distances of
+// magnitude >= 1e30 * |b - o|, beyond any ray length, or the right sign within 2^-24 |o|
+// of a slab plane — a margin away from the geometry.
 __device__ __forceinline__ bool obj_overlap(v3 oi, v3 inv, const StepObj& B, float tlim) {
     const float tx0 = __builtin_fmaf(B.bmin[0], inv.x, -oi.x), tx1 = __builtin_fmaf(B.bmax[0], inv.x, -oi.x);
     const float ty0 = __builtin_fmaf(B.bmin[1], inv.y, -oi.y), ty1 = __builtin_fmaf(B.bmax[1], inv.y, -oi.y);
@@ -209,10 +212,10 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
     W.ro[lane] = make_float4(o.x, o.y, o.z, kINF);
     W.rd[lane] = make_float4(d.x, d.y, d.z, 0.0f);
     v3 inv[R], oi[R];
-    inv[0] = rcp3(d);
+    inv[0] = rcp3c(d);
     oi[0] = o * inv[0];
 #pragma unroll
-    for (int l = 0; l < NL; ++l) inv[1 + l] = rcp3(sd[l]), oi[1 + l] = so[l] * inv[1 + l];
+    for (int l = 0; l < NL; ++l) inv[1 + l] = rcp3c(sd[l]), oi[1 + l] = so[l] * inv[1 + l];
     wave_sync();
     const int n = SO.n;
     for (int ob = 0; ob < n; ++ob) {
@@ -305,10 +308,10 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const D
     v3 inv[R], oi[R];
 #pragma unroll
     for (int q = 0; q < R; ++q) tm[q] = 0ull;
-    inv[0] = rcp3(d);
+    inv[0] = rcp3c(d);
     oi[0] = o * inv[0];
 #pragma unroll
-    for (int l = 0; l < NL; ++l) inv[1 + l] = rcp3(sd[l]), oi[1 + l] = so[l] * inv[1 + l];
+    for (int l = 0; l < NL; ++l) inv[1 + l] = rcp3c(sd[l]), oi[1 + l] = so[l] * inv[1 + l];
     for (int ob0 = 0; ob0 < n_objs; ob0 += G) {
         const int ob = ob0 + u;
         if (ob < n_objs) {
@@ -349,6 +352,92 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const D
     }
     best = group_min64<G>(bk);
     occ = group_or32<G>(oc);
+}
+
+// ------------------------------------------------- two-level trace, phase A ----
+// k_trace_2a (wavefront.hip) with the small objects traced by merged_trace's object-major
+// pair passes instead of a per-lane object loop: one wave = 64 slots, their extension ray
+// and shadow rays, the small objects' triangles in LDS (KParams::stri, iteration order, so
+// the (t bits << 32 | local index) minimum is the (t, original index) minimum).  The winner's
+// (t, u, v) are recomputed with Mesh::rayTriangleIntersect's ops as the merged kernel does;
+// rays whose segment reaches the BVH root are queued for k_trace_deep.
+template <int NL>
+__global__ __launch_bounds__(kBlock) void k_trace_2a_coop(KParams P, const StepObjs SO, const uint32_t* __restrict__ list,
+                                                          const uint32_t* __restrict__ count, uint32_t* zero_count) {
+    extern __shared__ __attribute__((aligned(16))) f4 lds_2c[];
+    LScene L;
+    L.tri = lds_2c;
+    MergedWave<NL>* Wv = reinterpret_cast<MergedWave<NL>*>(lds_2c + 3 * P.n_stri);
+    const int tid = threadIdx.x, lane = tid & 63;
+    MergedWave<NL>& W = Wv[tid >> 6];
+    lds_copy(const_cast<f4*>(L.tri), P.stri, 3 * P.n_stri, tid);
+    zero_parts(P, zero_count);
+    __syncthreads();
+    const f4 r0 = P.bvh_node[0], r1 = P.bvh_node[1], r2 = P.bvh_node[2], r3 = P.bvh_node[3];   // root
+    const PartIter it = part_iter(P, count, kBlock);
+    uint32_t* dq = P.deep + (size_t)it.p * P.deep_cap;
+    for (uint32_t base = it.first; base < it.n; base += it.stride) {
+        const uint32_t i = base + tid;
+        const bool valid = i < it.n;
+        const uint32_t s = valid ? list[it.p * P.part_cap + i] : 0;
+        const uint32_t st = valid ? P.state[s] : 0;
+        const bool want = (st & ST_RAY) != 0;
+        const uint32_t smask = (st >> ST_SHADOW_SHIFT) & ((1u << NL) - 1u);
+        v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+        if (want) o = xyz(P.ray_o[s]), d = xyz(P.ray_d[s]);
+        v3 so[NL + 1], sd[NL + 1];
+        float stm[NL + 1];
+#pragma unroll
+        for (int l = 0; l <= NL; ++l) so[l] = sd[l] = mk(0, 0, 0), stm[l] = 0.0f;
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+            if (smask & (1u << l)) {
+                const f4 a = P.sh_o[(size_t)l * P.n_slots + s];
+                so[l] = xyz(a), stm[l] = a.w;
+                sd[l] = xyz(P.sh_d[(size_t)l * P.n_slots + s]);
+            }
+            W.ro[(1 + l) * 64 + lane] = make_float4(so[l].x, so[l].y, so[l].z, stm[l]);
+            W.rd[(1 + l) * 64 + lane] = make_float4(sd[l].x, sd[l].y, sd[l].z, 0.0f);
+        }
+        unsigned long long best;
+        uint32_t occ;
+        merged_trace<NL>(SO, L, W, lane, want, o, d, smask, so, sd, stm, best, occ);
+        float bt = kINF, bu = 0.0f, bv = 0.0f;
+        int bk = -1;
+        if (want && best != ~0ull) {
+            const int hk = (int)(uint32_t)best;
+            (void)ray_tri(o, d, xyz(L.tri[3 * hk]), xyz(L.tri[3 * hk + 1]), xyz(L.tri[3 * hk + 2]), bt, bu, bv);
+            bk = __float_as_int(L.tri[3 * hk + 2].w);
+        }
+        const v3 inv = rcp3(d);
+        const bool dext = want && root_overlap(r0, r1, r2, r3, o, inv, bt);
+        uint32_t dsh = 0;
+#pragma unroll
+        for (int l = 0; l < NL; ++l)
+            if ((smask & ~occ & (1u << l)) && root_overlap(r0, r1, r2, r3, so[l], rcp3(sd[l]), stm[l])) dsh |= 1u << l;
+        if (valid) {
+            if (want) P.hit[s] = make_float4(bt, bu, bv, __int_as_float(bk));
+            if (smask) P.occ[s] = occ & smask;
+        }
+        wave_append(valid && dext, s * 8u, dq, P.deep_count + it.p, lane);
+#pragma unroll
+        for (int l = 0; l < NL; ++l)
+            wave_append(valid && ((dsh >> l) & 1u), s * 8u + 1u + (uint32_t)l, dq, P.deep_count + it.p, lane);
+        wave_sync();   // W is rewritten by the next round's rays
+    }
+}
+
+hipError_t launch_trace_2a_coop(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
+                                uint32_t blocks, hipStream_t st) {
+    if (P.n_lights <= 1) {
+        const size_t lds = (size_t)P.n_stri * 3 * sizeof(f4) + (kBlock / 64) * sizeof(MergedWave<1>);
+        hipLaunchKernelGGL((k_trace_2a_coop<1>), dim3(blocks), dim3(kBlock), lds, st, P, *P.sstep, list, count, zero);
+    } else {
+        const size_t lds = (size_t)P.n_stri * 3 * sizeof(f4) + (kBlock / 64) * sizeof(MergedWave<kMaxLights>);
+        hipLaunchKernelGGL((k_trace_2a_coop<kMaxLights>), dim3(blocks), dim3(kBlock), lds, st, P, *P.sstep, list, count,
+                           zero);
+    }
+    return hipGetLastError();
 }
 
 // --------------------------------------------------------------- RNG refills ----
@@ -530,7 +619,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
 #endif
     zero_parts(P, zero_count);
     const PartIter it = part_iter(P, count, (kBlock / 64) * SPW);
-    const uint32_t spp = P.spp, max_depth = P.max_depth, width = P.width, height = P.height;
+    const uint32_t spp = P.spp, max_depth = P.max_depth, width = P.width;
     for (uint32_t base = it.first; base < it.n; base += it.stride) {
         const uint32_t i = base + (uint32_t)(tid >> 6) * SPW + (uint32_t)lane / G;
         const bool own = lane / G < SPW && i < it.n;

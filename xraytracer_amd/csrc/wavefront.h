@@ -115,6 +115,7 @@ constexpr int kBvhMaxDepth = 48;      // BVH build: depth bound (SAH above max -
 constexpr int kBvhStack = 24;         // k_trace_bvh: LDS traversal stack entries per thread (> tree depth)
 constexpr int kSphBvhMin = 16;        // sphere scenes with at least this many spheres get a skip-link BVH
 constexpr int kSmallTris = 1024;   // scenes up to this size keep every triangle in LDS
+constexpr int kLargeObjTris = 256;  // two-level trace: mesh objects above this go into the BVH
 constexpr int kSmallObjs = 256;
 constexpr unsigned kStepLds = 64u * 1024u;   // LDS budget of the fused schedule (k_step)
 
@@ -162,6 +163,19 @@ struct KParams {
     const f4* bvh_tri;        // triangles in BVH leaf order, as `tri` but e2.w = original index
     int bvh_stack;            // k_trace_bvh: LDS stack entries per thread (tree depth + 1 <= kBvhStack)
     int bvh_nodes;            // BvhNode count
+    // two-level trace of large triangle scenes (C4): objects of at most kLargeObjTris
+    // triangles are scanned directly (k_trace_2a: LDS, culling boxes and planes); only rays
+    // whose segment reaches the BVH over the large objects' triangles are queued for it
+    // (k_trace_deep)
+    const f4* stri;           // small objects' triangles, as bvh_tri (e2.w = original index)
+    const DObjBox* sbox;      // their culling boxes (first / count into stri)
+    const DObjPlane* splane;
+    int n_stri, n_sobj, two_level;
+    const struct StepObjs* sstep;   // HOST pointer (launch_trace passes it by value): the small objects as
+                                    // merged-trace records when n_sobj <= kMergedMaxObjs, else null
+    uint32_t* deep;           // queued rays (slot * 8 + kind: 0 extension, 1 + l shadow ray l), per partition
+    uint32_t* deep_count;     // [kMaxParts] counts, then [kMaxParts] fetch counters
+    uint32_t deep_cap;        // entries per partition
     const f4* snode;          // sphere scenes: threaded BVH (bvh.h SkipNode, 2 f4 each), else null
     const f4* ssph;           // spheres in BVH leaf order (center, radius)
     const int* sbk;           // per ssph entry: original sphere index | (occluder << 30)

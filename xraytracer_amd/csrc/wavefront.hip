@@ -237,16 +237,6 @@ __device__ __forceinline__ bool bvh_leaf(const KParams& P, int first, int count,
     return false;
 }
 
-// entry distance of the ray segment [0, tlim] into a padded node box, +inf if it misses
-__device__ __forceinline__ float bvh_enter(const f4& mn, const f4& mx, v3 o, v3 inv, float tlim) {
-    const float tx0 = (mn.x - o.x) * inv.x, tx1 = (mx.x - o.x) * inv.x;
-    const float ty0 = (mn.y - o.y) * inv.y, ty1 = (mx.y - o.y) * inv.y;
-    const float tz0 = (mn.z - o.z) * inv.z, tz1 = (mx.z - o.z) * inv.z;
-    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
-    return tn > tf ? __builtin_inff() : tn;
-}
-
 // ANY: returns occluded; else fills (bt, bu, bv, bk) (bk = -1: miss).  Closest-hit rays
 // descend into the nearer child first (entry distance) and stack the farther one, so the
 // best t shrinks early and culls more of the tree; the result does not depend on the
@@ -335,6 +325,257 @@ __global__ __launch_bounds__(kBlock) void k_trace_bvh(KParams P, const uint32_t*
                     occ |= 1u << l;
             }
             P.occ[s] = occ;
+        }
+    }
+}
+
+// ============================================================ two-level trace ====
+// Large triangle scenes with small objects beside the big meshes (C4: the Cornell walls and
+// blocks around a 51,200-triangle sphere): one wave's rays mostly bounce between the small
+// objects, but a single lane whose segment passes the big mesh makes the whole wave walk
+// its BVH (k_trace_bvh: lane utilisation 0.12).  Phase A (k_trace_2a) scans the small
+// objects as k_trace_small does (LDS, in iteration order, strict t < best: the
+// lexicographic (t, index) minimum among them), then queues only the rays whose segment
+// [0, best t] (any-hit: [0, tmax], if not yet occluded) overlaps the BVH root; phase B
+// (k_trace_deep) walks the BVH for the queued rays alone — full waves of deep rays — and
+// merges with the same (t, index) order (bvh_leaf).  The result is the one-level trace's.
+__device__ __forceinline__ bool plane_away_w(v3 o, v3 d, const DObjPlane& pl) {   // step_tri.hip plane_away
+    const float oa = pl.axis == 0 ? o.x : (pl.axis == 1 ? o.y : o.z);
+    const float da = pl.axis == 0 ? d.x : (pl.axis == 1 ? d.y : d.z);
+    return pl.axis >= 0 && (oa - pl.c) * da >= 0.0f;
+}
+
+template <int NL>
+__global__ __launch_bounds__(kBlock) void k_trace_2a(KParams P, const uint32_t* __restrict__ list,
+                                                     const uint32_t* __restrict__ count, uint32_t* zero_count) {
+    extern __shared__ __attribute__((aligned(16))) f4 lds_2a[];
+    f4* ltri = lds_2a;
+    DObjBox* lbox = reinterpret_cast<DObjBox*>(lds_2a + 3 * P.n_stri);
+    DObjPlane* lpl = reinterpret_cast<DObjPlane*>(lbox + P.n_sobj);
+    zero_parts(P, zero_count);
+    const int tid = threadIdx.x, lane = tid & 63;
+    for (int q = tid; q < 3 * P.n_stri; q += kBlock) ltri[q] = P.stri[q];
+    for (int q = tid; q < P.n_sobj; q += kBlock) lbox[q] = P.sbox[q], lpl[q] = P.splane[q];
+    __syncthreads();
+    const f4 r0 = P.bvh_node[0], r1 = P.bvh_node[1], r2 = P.bvh_node[2], r3 = P.bvh_node[3];   // root
+    const PartIter it = part_iter(P, count, kBlock);
+    uint32_t* dq = P.deep + (size_t)it.p * P.deep_cap;
+    for (uint32_t base = it.first; base < it.n; base += it.stride) {
+        const uint32_t i = base + tid;
+        const bool valid = i < it.n;
+        const uint32_t s = valid ? list[it.p * P.part_cap + i] : 0;
+        const uint32_t st = valid ? P.state[s] : 0;
+        const bool want = (st & ST_RAY) != 0;
+        const uint32_t smask = (st >> ST_SHADOW_SHIFT) & ((1u << NL) - 1u);
+        v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
+        if (want) {
+            o = xyz(P.ray_o[s]);
+            d = xyz(P.ray_d[s]);
+        }
+        v3 so[NL], sd[NL];
+        float stmax[NL];
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+            so[l] = mk(0, 0, 0), sd[l] = mk(0, 0, 0), stmax[l] = 0.0f;
+            if (smask & (1u << l)) {
+                const f4 a = P.sh_o[(size_t)l * P.n_slots + s];
+                so[l] = xyz(a);
+                stmax[l] = a.w;
+                sd[l] = xyz(P.sh_d[(size_t)l * P.n_slots + s]);
+            }
+        }
+        const v3 inv = rcp3(d);
+        uint32_t occ = 0;
+        float best_t = kINF, bu = 0.0f, bv = 0.0f;
+        int best = -1;
+        for (int ob = 0; ob < P.n_sobj; ++ob) {
+            const DObjBox B = lbox[ob];
+            const DObjPlane pl = lpl[ob];
+            const int cnt = B.count_occ & 0x7fffffff;
+            const bool occluder = B.count_occ < 0;
+            const bool ne = want && !plane_away_w(o, d, pl) && box_overlap(o, inv, B, best_t);
+            uint32_t nsm = 0;
+            if (occluder) {
+#pragma unroll
+                for (int l = 0; l < NL; ++l)
+                    if ((smask & ~occ & (1u << l)) && !plane_away_w(so[l], sd[l], pl) &&
+                        box_overlap(so[l], rcp3(sd[l]), B, stmax[l]))
+                        nsm |= 1u << l;
+            }
+            if (__ballot(ne || nsm) == 0) continue;
+            for (int k = B.first; k < B.first + cnt; ++k) {
+                const v3 v0 = xyz(ltri[3 * k]), e1 = xyz(ltri[3 * k + 1]);
+                const f4 E2 = ltri[3 * k + 2];
+                const v3 e2 = xyz(E2);
+                if (ne) {
+                    float t, u, v;
+                    if (ray_tri(o, d, v0, e1, e2, t, u, v) && t < best_t)
+                        best_t = t, bu = u, bv = v, best = __float_as_int(E2.w);
+                }
+#pragma unroll
+                for (int l = 0; l < NL; ++l) {
+                    if (nsm & ~occ & (1u << l)) {
+                        float t, u, v;
+                        if (ray_tri(so[l], sd[l], v0, e1, e2, t, u, v) && t < stmax[l]) occ |= 1u << l;
+                    }
+                }
+            }
+        }
+        const bool dext = want && root_overlap(r0, r1, r2, r3, o, inv, best_t);
+        uint32_t dsh = 0;
+#pragma unroll
+        for (int l = 0; l < NL; ++l)
+            if ((smask & ~occ & (1u << l)) && root_overlap(r0, r1, r2, r3, so[l], rcp3(sd[l]), stmax[l])) dsh |= 1u << l;
+        if (valid) {
+            if (want) P.hit[s] = make_float4(best_t, bu, bv, __int_as_float(best));
+            if (smask) P.occ[s] = occ;
+        }
+        wave_append(valid && dext, s * 8u, dq, P.deep_count + it.p, lane);
+#pragma unroll
+        for (int l = 0; l < NL; ++l)
+            wave_append(valid && ((dsh >> l) & 1u), s * 8u + 1u + (uint32_t)l, dq, P.deep_count + it.p, lane);
+    }
+}
+
+template <int NL, typename SE>
+__global__ __launch_bounds__(kBlock) void k_trace_deep(KParams P) {
+    extern __shared__ uint32_t bvh_stack_lds[];
+    const int tid = threadIdx.x;
+    const int ntop = P.bvh_nodes < (int)kBvhTopNodes ? P.bvh_nodes : (int)kBvhTopNodes;
+    f4* top = reinterpret_cast<f4*>(bvh_stack_lds);
+    for (int q = tid; q < 4 * ntop; q += kBlock) top[q] = P.bvh_node[q];
+    SE* stack = reinterpret_cast<SE*>(bvh_stack_lds + 16 * ntop);
+    __syncthreads();
+    const PartIter it = part_iter(P, P.deep_count, kBlock);
+    const uint32_t* dq = P.deep + (size_t)it.p * P.deep_cap;
+    SE* stk = stack + tid;
+    for (uint32_t base = it.first; base < it.n; base += it.stride) {
+        const uint32_t i = base + tid;
+        if (i >= it.n) continue;
+        const uint32_t e = dq[i], s = e >> 3, kind = e & 7u;
+        if (kind == 0) {
+            const f4 h = P.hit[s];
+            float bt = h.x, bu = h.y, bv = h.z;
+            int bk = __float_as_int(h.w);
+            (void)bvh_trace<false, SE>(P, top, ntop, stk, xyz(P.ray_o[s]), xyz(P.ray_d[s]), kINF, bt, bu, bv, bk);
+            P.hit[s] = make_float4(bt, bu, bv, __int_as_float(bk));
+        } else {
+            const uint32_t l = kind - 1u;
+            const f4 a = P.sh_o[(size_t)l * P.n_slots + s];
+            float bt = kINF, bu, bv;
+            int bk = -1;
+            if (bvh_trace<true, SE>(P, top, ntop, stk, xyz(a), xyz(P.sh_d[(size_t)l * P.n_slots + s]), a.w, bt, bu, bv, bk))
+                atomicOr(P.occ + s, 1u << l);
+        }
+    }
+}
+
+// Phase B with dynamic ray fetch.  In k_trace_deep a wave holds its 64 rays until the
+// longest traversal ends (measured lane utilisation 0.095: most queued rays cross the mesh's
+// box and leave after a few nodes, a few descend to the surface).  Here a lane whose ray is
+// done takes the next queued ray of its partition (one atomic per wave per refill, when at
+// least 16 lanes are idle or the wave is empty), so lanes stay busy until the queue drains.
+// One loop iteration = one node of each active lane's traversal (bvh_trace's step: both
+// children tested, leaves first, nearer interior child next, farther one stacked); closest
+// hits keep bvh_leaf's (t, index) order, any-hit rays stop at the first occluder.
+template <typename SE>
+__global__ __launch_bounds__(kBlock) void k_trace_deep_pt(KParams P) {
+    extern __shared__ uint32_t bvh_stack_lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int ntop = P.bvh_nodes < (int)kBvhTopNodes ? P.bvh_nodes : (int)kBvhTopNodes;
+    f4* top = reinterpret_cast<f4*>(bvh_stack_lds);
+    for (int q = tid; q < 4 * ntop; q += kBlock) top[q] = P.bvh_node[q];
+    SE* stk = reinterpret_cast<SE*>(bvh_stack_lds + 16 * ntop) + tid;
+    __syncthreads();
+    const uint32_t p = blockIdx.x % P.n_part;
+    const uint32_t cnt = P.deep_count[p];
+    uint32_t* next_ctr = P.deep_count + kMaxParts + p;
+    const uint32_t* dq = P.deep + (size_t)p * P.deep_cap;
+    bool active = false, drained = cnt == 0, any = false;
+    uint32_t s = 0, l = 0;
+    int node = 0, sp = 0, bk = -1;
+    v3 o = mk(0, 0, 0), d = mk(0, 0, 0), inv = mk(0, 0, 0);
+    float tmax = 0.0f, bt = kINF, bu = 0.0f, bv = 0.0f;
+    while (true) {
+        const uint64_t idle = __ballot(!active);
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        if (!drained && (nidle >= 16u || nidle == 64u)) {
+            const int leader = __ffsll((unsigned long long)idle) - 1;
+            uint32_t b = 0;
+            if (lane == leader) b = atomicAdd(next_ctr, nidle);
+            b = (uint32_t)__builtin_amdgcn_readlane((int)b, leader);
+            if (b + nidle >= cnt) drained = true;
+            if (!active) {
+                const uint32_t idx = b + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                if (idx < cnt) {
+                    const uint32_t e = dq[idx];
+                    s = e >> 3;
+                    const uint32_t kind = e & 7u;
+                    any = kind != 0;
+                    if (!any) {
+                        o = xyz(P.ray_o[s]), d = xyz(P.ray_d[s]);
+                        const f4 h = P.hit[s];
+                        bt = h.x, bu = h.y, bv = h.z, bk = __float_as_int(h.w);
+                        tmax = kINF;
+                    } else {
+                        l = kind - 1u;
+                        const f4 a = P.sh_o[(size_t)l * P.n_slots + s];
+                        o = xyz(a), tmax = a.w;
+                        d = xyz(P.sh_d[(size_t)l * P.n_slots + s]);
+                        bt = kINF, bk = -1;
+                    }
+                    inv = rcp3(d);
+                    node = 0, sp = 0;
+                    active = true;
+                }
+            }
+        }
+        if (!__ballot(active)) break;
+        if (!active) continue;
+        f4 n0, n1, n2, n3;
+        if (node < ntop) {
+            const f4* N = top + 4 * node;
+            n0 = N[0], n1 = N[1], n2 = N[2], n3 = N[3];
+        } else {
+            const f4* N = P.bvh_node + 4 * (size_t)node;
+            n0 = N[0], n1 = N[1], n2 = N[2], n3 = N[3];
+        }
+        const float lim = any ? tmax : bt;
+        const int lcount = __float_as_int(n1.w), rcount = __float_as_int(n3.w);
+        const float el = lcount >= 0 ? bvh_enter(n0, n1, o, inv, lim) : __builtin_inff();
+        const float er = rcount >= 0 ? bvh_enter(n2, n3, o, inv, lim) : __builtin_inff();
+        const bool hl = el != __builtin_inff(), hr = er != __builtin_inff();
+        bool occluded = false;
+        // leaves first (either order gives the same result)
+        if (hl && lcount > 0) {
+            occluded = any ? bvh_leaf<true>(P, __float_as_int(n0.w), lcount, o, d, tmax, bt, bu, bv, bk)
+                           : bvh_leaf<false>(P, __float_as_int(n0.w), lcount, o, d, tmax, bt, bu, bv, bk);
+        }
+        if (!occluded && hr && rcount > 0) {
+            occluded = any ? bvh_leaf<true>(P, __float_as_int(n2.w), rcount, o, d, tmax, bt, bu, bv, bk)
+                           : bvh_leaf<false>(P, __float_as_int(n2.w), rcount, o, d, tmax, bt, bu, bv, bk);
+        }
+        bool done = occluded;
+        if (!done) {
+            const bool il = hl && lcount == 0, ir = hr && rcount == 0;
+            int nx = -1;
+            if (il && ir) {
+                const bool lfirst = any || el <= er;
+                nx = __float_as_int(lfirst ? n0.w : n2.w);
+                stk[(sp++) * kBlock] = (SE)__float_as_int(lfirst ? n2.w : n0.w);
+            } else if (il) {
+                nx = __float_as_int(n0.w);
+            } else if (ir) {
+                nx = __float_as_int(n2.w);
+            }
+            if (nx >= 0) node = nx;
+            else if (sp == 0) done = true;
+            else node = (int)stk[(--sp) * kBlock];
+        }
+        if (done) {
+            if (!any) P.hit[s] = make_float4(bt, bu, bv, __int_as_float(bk));
+            else if (occluded) atomicOr(P.occ + s, 1u << l);
+            active = false;
         }
     }
 }
@@ -2173,12 +2414,33 @@ hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* 
         const bool small = P.bvh_nodes <= 0x10000;
         const size_t ntop = std::min<size_t>((size_t)P.bvh_nodes, kBvhTopNodes);
         const size_t lds = ntop * 4 * sizeof(f4) + (size_t)P.bvh_stack * kBlock * (small ? sizeof(uint16_t) : sizeof(uint32_t));
-        if (small && P.n_lights <= 1)
+        const bool nl1 = P.n_lights <= 1;
+        if (P.two_level) {
+            if (!P.deep || !P.deep_count) return hipErrorInvalidValue;
+            hipError_t e = hipMemsetAsync(P.deep_count, 0, 2 * kMaxParts * sizeof(uint32_t), st);   // counts, fetch counters
+            if (e != hipSuccess) return e;
+            const size_t lds_a = (size_t)P.n_stri * 3 * sizeof(f4) + (size_t)P.n_sobj * (sizeof(DObjBox) + sizeof(DObjPlane));
+            if (P.sstep)
+                e = launch_trace_2a_coop(P, list, count, zero, blocks, st);
+            else if (nl1)
+                hipLaunchKernelGGL((k_trace_2a<1>), dim3(blocks), dim3(kBlock), lds_a, st, P, list, count, zero);
+            else
+                hipLaunchKernelGGL((k_trace_2a<kMaxLights>), dim3(blocks), dim3(kBlock), lds_a, st, P, list, count, zero);
+            if (e == hipSuccess) e = hipGetLastError();
+            if (e != hipSuccess) return e;
+            // persistent: up to 2048 blocks (8 per CU), each serving partition blockIdx % n_part
+            const uint32_t db = P.n_part * std::max<uint32_t>(1u, std::min<uint32_t>(2048u / P.n_part,
+                                                                                    (P.deep_cap + kBlock - 1) / kBlock));
+            if (small) hipLaunchKernelGGL((k_trace_deep_pt<uint16_t>), dim3(db), dim3(kBlock), lds, st, P);
+            else hipLaunchKernelGGL((k_trace_deep_pt<uint32_t>), dim3(db), dim3(kBlock), lds, st, P);
+            return hipGetLastError();
+        }
+        if (small && nl1)
             hipLaunchKernelGGL((k_trace_bvh<1, uint16_t>), dim3(blocks), dim3(kBlock), lds, st, P, list, count, zero);
         else if (small)
             hipLaunchKernelGGL((k_trace_bvh<kMaxLights, uint16_t>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
                                zero);
-        else if (P.n_lights <= 1)
+        else if (nl1)
             hipLaunchKernelGGL((k_trace_bvh<1, uint32_t>), dim3(blocks), dim3(kBlock), lds, st, P, list, count, zero);
         else
             hipLaunchKernelGGL((k_trace_bvh<kMaxLights, uint32_t>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,

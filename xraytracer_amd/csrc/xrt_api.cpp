@@ -41,14 +41,15 @@ struct xrt_ctx {
     // scene
     std::vector<DevBuf*> scene_bufs;
     DevBuf tri, tri_ng, tri_nrm, sph, sph_obj, box, objs, lights, segs, density, obj_box, obj_plane, bvh_node,
-        bvh_tri, snode, ssph, sbk;
+        bvh_tri, snode, ssph, sbk, stri, sbox, splane;
     KParams base{};
     StepObjs step_objs{};   // kernel-argument object records of the merged-trace schedule
+    StepObjs sstep{};       // two-level trace: the small objects' records (KParams::sstep)
     bool has_scene = false, has_camera = false, has_medium = false;
     // slots
     size_t cap_slots = 0;
     DevBuf ray_o, ray_d, thr, rad, thr_prev, hit, hit2, hit3, sh_o, sh_d, sh_c, med, med2, nee;
-    DevBuf state, sample_k, depth, occ, rng_c, rng_g, ring, c_seg, c_shadow, c_rej, c_stall, lists;
+    DevBuf state, sample_k, depth, occ, rng_c, rng_g, ring, c_seg, c_shadow, c_rej, c_stall, lists, deep;
     DevBuf counts, stats, fb, scratch, kparams;
     size_t cap_fb = 0;
     uint32_t* h_poll = nullptr;  // pinned
@@ -116,6 +117,20 @@ T* as(DevBuf& b) {
 }
 
 uint32_t shard_rows(uint32_t h, uint32_t idx, uint32_t n) { return idx < h ? (h - idx + n - 1) / n : 0; }
+
+// two-level trace queues (KParams::deep): per partition part_cap * (1 + lights) entries, then
+// kMaxParts counts and kMaxParts fetch counters (k_trace_deep_pt)
+int setup_deep(xrt_ctx* c, KParams& P) {
+    P.deep = nullptr, P.deep_count = nullptr, P.deep_cap = 0;
+    if (!P.two_level) return XRT_OK;
+    P.deep_cap = P.part_cap * (1u + (uint32_t)P.n_lights);
+    const size_t words = (size_t)P.n_part * P.deep_cap + 2 * kMaxParts;   // queues, counts, fetch counters
+    const int rc = ensure(c, c->deep, words * 4);
+    if (rc) return rc;
+    P.deep = as<uint32_t>(c->deep);
+    P.deep_count = P.deep + (size_t)P.n_part * P.deep_cap;
+    return XRT_OK;
+}
 
 // Is the device's div_const(x, c, RN(1/c)) — q = x * rc, q + (x - c q) * rc with two fmas —
 // equal to the IEEE quotient x / c for every x it is used on?  Within div_const's window
@@ -211,6 +226,7 @@ void xrt_destroy(xrt_ctx* c) {
                      &c->sample_k, &c->depth, &c->occ, &c->rng_c, &c->rng_g, &c->ring, &c->c_seg, &c->c_shadow,
                      &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch, &c->kparams};
     for (DevBuf* b : all) free_buf(*b);
+    free_buf(c->stri), free_buf(c->sbox), free_buf(c->splane), free_buf(c->deep);
     free_buf(c->stage), free_buf(c->q_rays), free_buf(c->q_tmax), free_buf(c->q_out);
     free_buf(c->brick_table), free_buf(c->brick_data);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
@@ -395,27 +411,88 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
     // Margin: 1e-4 of the scene diagonal + 1e-4, above the float error of a Moller-Trumbore
     // hit position, so box tests never drop a hit the linear scan accepts.
     P.bvh_node = nullptr, P.bvh_tri = nullptr, P.bvh_stack = 0, P.bvh_nodes = 0;
+    P.stri = nullptr, P.sbox = nullptr, P.splane = nullptr, P.n_stri = 0, P.n_sobj = 0, P.two_level = 0;
+    P.sstep = nullptr;
     if (P.scene_kind == SCN_TRI && !P.small_tri && P.n_tris > 0 && !exp_env("XRT_NO_BVH")) {
-        const size_t nt = (size_t)P.n_tris;
+        // two-level split: mesh objects of more than kLargeObjTris triangles go into the BVH,
+        // the rest (if any, and if they fit the LDS scan) are scanned directly
+        std::vector<uint32_t> big;   // original indices of the BVH's triangles
+        std::vector<DObjBox> sboxes;
+        std::vector<DObjPlane> splanes;
+        std::vector<f4> stri;
+        {
+            int t0 = 0;
+            for (size_t k = 0; k < objs.size(); ++k) {
+                const int cnt = s->objects[k].count;
+                if (cnt > kLargeObjTris) {
+                    for (int t = t0; t < t0 + cnt; ++t) big.push_back((uint32_t)t);
+                } else if (cnt > 0) {
+                    DObjBox b;
+                    b.first = (int)(stri.size() / 3);
+                    b.count_occ = cnt | (objs[k].light < 0 ? (int)0x80000000 : 0);
+                    for (int t = t0; t < t0 + cnt; ++t) {
+                        stri.push_back(tri[3 * t]), stri.push_back(tri[3 * t + 1]), stri.push_back(tri[3 * t + 2]);
+                        stri.back().w = bits(t);
+                    }
+                    sboxes.push_back(b);
+                    splanes.push_back(planes[k]);
+                }
+                t0 += cnt;
+            }
+        }
+        const bool two = !big.empty() && !sboxes.empty() && stri.size() / 3 <= (size_t)kSmallTris &&
+                         sboxes.size() <= (size_t)kSmallObjs && !exp_env("XRT_NO_TWO_LEVEL");
+        if (!two) {
+            big.resize(P.n_tris);
+            for (size_t t = 0; t < big.size(); ++t) big[t] = (uint32_t)t;
+        }
+        const size_t nt = big.size();
         std::vector<float> mn(3 * nt), mx(3 * nt);
         float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-        for (size_t t = 0; t < nt; ++t) {
+        auto tri_box = [&](size_t t, float* bmn, float* bmx) {
             const f4 v0 = tri[3 * t], e1 = tri[3 * t + 1], e2 = tri[3 * t + 2];
             const float vs[3][3] = {{v0.x, v0.y, v0.z}, {v0.x + e1.x, v0.y + e1.y, v0.z + e1.z},
                                     {v0.x + e2.x, v0.y + e2.y, v0.z + e2.z}};
             for (int q = 0; q < 3; ++q) {
-                mn[3 * t + q] = std::min({vs[0][q], vs[1][q], vs[2][q]});
-                mx[3 * t + q] = std::max({vs[0][q], vs[1][q], vs[2][q]});
-                lo[q] = std::min(lo[q], mn[3 * t + q]), hi[q] = std::max(hi[q], mx[3 * t + q]);
+                bmn[q] = std::min({vs[0][q], vs[1][q], vs[2][q]});
+                bmx[q] = std::max({vs[0][q], vs[1][q], vs[2][q]});
+                lo[q] = std::min(lo[q], bmn[q]), hi[q] = std::max(hi[q], bmx[q]);
+            }
+        };
+        for (size_t i = 0; i < nt; ++i) tri_box(big[i], &mn[3 * i], &mx[3 * i]);
+        if (two) {   // small objects' boxes (the scene diagonal covers them too)
+            for (DObjBox& b : sboxes) {
+                for (int q = 0; q < 3; ++q) b.bmin[q] = 3e38f, b.bmax[q] = -3e38f;
+                for (int i = b.first; i < b.first + (b.count_occ & 0x7fffffff); ++i) {
+                    float bmn[3], bmx[3];
+                    tri_box((size_t)__builtin_bit_cast(int, stri[3 * i + 2].w), bmn, bmx);
+                    for (int q = 0; q < 3; ++q) b.bmin[q] = std::min(b.bmin[q], bmn[q]), b.bmax[q] = std::max(b.bmax[q], bmx[q]);
+                }
             }
         }
         const float diag = std::sqrt((hi[0] - lo[0]) * (hi[0] - lo[0]) + (hi[1] - lo[1]) * (hi[1] - lo[1]) +
                                      (hi[2] - lo[2]) * (hi[2] - lo[2]));
+        if (two) {
+            // culling margin of the small-scene scan (1e-3 of the diagonal + 1e-3, see above)
+            const float margin = 1e-3f * diag + 1e-3f;
+            for (DObjBox& b : sboxes)
+                for (int q = 0; q < 3; ++q) b.bmin[q] -= margin, b.bmax[q] += margin;
+            if ((rc = upload(c, c->stri, stri.data(), stri.size() * sizeof(f4))) ||
+                (rc = upload(c, c->sbox, sboxes.data(), sboxes.size() * sizeof(DObjBox))) ||
+                (rc = upload(c, c->splane, splanes.data(), splanes.size() * sizeof(DObjPlane))))
+                return rc;
+            P.stri = as<f4>(c->stri), P.sbox = as<DObjBox>(c->sbox), P.splane = as<DObjPlane>(c->splane);
+            P.n_stri = (int)(stri.size() / 3), P.n_sobj = (int)sboxes.size(), P.two_level = 1;
+            if (sboxes.size() <= (size_t)kMergedMaxObjs) {   // phase A as cooperative pair passes
+                build_step_objs(sboxes.data(), splanes.data(), (int)sboxes.size(), c->sstep);
+                P.sstep = &c->sstep;
+            }
+        }
         const BvhBuild B = build_bvh(mn.data(), mx.data(), (uint32_t)nt, kBvhLeaf, 1e-4f * diag + 1e-4f, kBvhMaxDepth);
         if (B.depth >= kBvhStack) return set_err(c, XRT_ERR_UNSUPPORTED, "BVH deeper than the traversal stack");
         std::vector<f4> btri(3 * nt);
         for (size_t i = 0; i < nt; ++i) {
-            const uint32_t t = B.order[i];
+            const uint32_t t = big[B.order[i]];
             btri[3 * i] = tri[3 * t], btri[3 * i + 1] = tri[3 * t + 1], btri[3 * i + 2] = tri[3 * t + 2];
             btri[3 * i + 2].w = bits((int)t);
         }
@@ -659,6 +736,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     P.c_stall = as<uint32_t>(c->c_stall);
     P.fb = fb;
     P.stats = as<unsigned long long>(c->stats);
+    if ((rc = setup_deep(c, P))) return rc;
 
     uint32_t* lists[2] = {as<uint32_t>(c->lists), as<uint32_t>(c->lists) + lcap};
     P.req = as<uint32_t>(c->lists) + 2 * lcap;
@@ -1051,6 +1129,7 @@ int xrt_query(xrt_ctx* c, uint32_t n, const float* rays, const float* tmax, int3
     P.ray_o = as<f4>(c->ray_o), P.ray_d = as<f4>(c->ray_d), P.hit = as<f4>(c->hit), P.hit2 = as<f4>(c->hit2);
     P.hit3 = as<f4>(c->hit3), P.sh_o = as<f4>(c->sh_o), P.sh_d = as<f4>(c->sh_d);
     P.state = as<uint32_t>(c->state), P.occ = as<uint32_t>(c->occ);
+    if ((rc = setup_deep(c, P))) return rc;
     HIPCHK(c, hipMemcpyAsync(c->q_rays.p, rays, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
     if (tmax) HIPCHK(c, hipMemcpyAsync(c->q_tmax.p, tmax, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
     uint32_t* cnt = as<uint32_t>(c->counts);
