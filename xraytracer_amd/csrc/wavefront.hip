@@ -675,50 +675,73 @@ __device__ __forceinline__ float brick_value(const DMedium& M, int i, int j, int
     const int b = M.brick_table[((k >> 3) * M.nby + (j >> 3)) * M.nbx + (i >> 3)];
     return b < 0 ? 0.0f : M.bricks[(size_t)b * 512 + (((k & 7) * 8 + (j & 7)) * 8 + (i & 7))];
 }
-__device__ float medium_density(const DMedium& M, v3 p) {
+// OpenVDB BoxSampler cell of a world position: index-space coordinates in double, the
+// lower corner (i, j, k) and the fractional weights
+struct VdbCell {
+    double u, v, w;
+    int i, j, k;
+};
+__device__ __forceinline__ VdbCell vdb_cell(const DMedium& M, v3 p) {
     const double inv = M.inv_voxel;
     const double xi = ((double)p.x - (double)M.origin[0]) * inv;
     const double yi = ((double)p.y - (double)M.origin[1]) * inv;
     const double zi = ((double)p.z - (double)M.origin[2]) * inv;
     const double fx = __builtin_floor(xi), fy = __builtin_floor(yi), fz = __builtin_floor(zi);
-    const int i = (int)fx, j = (int)fy, k = (int)fz;
-    const double u = xi - fx, v = yi - fy, w = zi - fz;
-    float d000, d001, d010, d011, d100, d101, d110, d111;
+    VdbCell C;
+    C.i = (int)fx, C.j = (int)fy, C.k = (int)fz;
+    C.u = xi - fx, C.v = yi - fy, C.w = zi - fz;
+    return C;
+}
+// dense grid, all eight corners inside: the x-neighbours are adjacent words, four dword-aligned
+// dwordx2 loads, corners in the order d000 d001 d010 d011 d100 d101 d110 d111
+__device__ __forceinline__ bool dense_interior(const DMedium& M, const VdbCell& C) {
+    return !M.brick_table && C.i >= 0 && C.j >= 0 && C.k >= 0 && C.i + 1 < M.nx && C.j + 1 < M.ny && C.k + 1 < M.nz;
+}
+__device__ __forceinline__ void dense_corners(const DMedium& M, const VdbCell& C, float (&q)[8]) {
+    typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+    using g2 = __attribute__((address_space(1))) const f2u;
+    const float* b = M.density + ((size_t)C.k * M.ny + (size_t)C.j) * M.nx + (size_t)C.i;
+    const size_t sy = (size_t)M.nx, sz = (size_t)M.nx * M.ny;
+    const f2u a = *(g2*)b, c = *(g2*)(b + sz), e = *(g2*)(b + sy), f = *(g2*)(b + sy + sz);
+    q[0] = a.x, q[4] = a.y, q[1] = c.x, q[5] = c.y, q[2] = e.x, q[6] = e.y, q[3] = f.x, q[7] = f.y;
+}
+__device__ __forceinline__ float vdb_interp(const DMedium& M, const VdbCell& C, const float (&q)[8]) {
+    const float g = vdb_lerp(vdb_lerp(vdb_lerp(q[0], q[1], C.w), vdb_lerp(q[2], q[3], C.w), C.v),
+                             vdb_lerp(vdb_lerp(q[4], q[5], C.w), vdb_lerp(q[6], q[7], C.w), C.v), C.u);
+    return M.multiplier * g;   // HeterogeneousMedium::getDensity (Src/medium.cpp:24-27)
+}
+
+__device__ float medium_density(const DMedium& M, v3 p) {
+    const VdbCell C = vdb_cell(M, p);
+    const int i = C.i, j = C.j, k = C.k;
+    float q[8];
     if (M.brick_table) {
         // a cell inside one brick: one table lookup, x-neighbours adjacent in the brick
         if (i >= 0 && j >= 0 && k >= 0 && i + 1 < M.nx && j + 1 < M.ny && k + 1 < M.nz && (i & 7) != 7 &&
             (j & 7) != 7 && (k & 7) != 7) {
             const int b = M.brick_table[((k >> 3) * M.nby + (j >> 3)) * M.nbx + (i >> 3)];
             if (b < 0) {
-                d000 = d001 = d010 = d011 = d100 = d101 = d110 = d111 = 0.0f;
+                for (int c = 0; c < 8; ++c) q[c] = 0.0f;
             } else {
-                const float* q = M.bricks + (size_t)b * 512 + (((k & 7) * 8 + (j & 7)) * 8 + (i & 7));
-                d000 = q[0], d100 = q[1], d010 = q[8], d110 = q[9];
-                d001 = q[64], d101 = q[65], d011 = q[72], d111 = q[73];
+                const float* r = M.bricks + (size_t)b * 512 + (((k & 7) * 8 + (j & 7)) * 8 + (i & 7));
+                q[0] = r[0], q[4] = r[1], q[2] = r[8], q[6] = r[9];
+                q[1] = r[64], q[5] = r[65], q[3] = r[72], q[7] = r[73];
             }
         } else {
-            d000 = brick_value(M, i, j, k), d001 = brick_value(M, i, j, k + 1);
-            d010 = brick_value(M, i, j + 1, k), d011 = brick_value(M, i, j + 1, k + 1);
-            d100 = brick_value(M, i + 1, j, k), d101 = brick_value(M, i + 1, j, k + 1);
-            d110 = brick_value(M, i + 1, j + 1, k), d111 = brick_value(M, i + 1, j + 1, k + 1);
+            q[0] = brick_value(M, i, j, k), q[1] = brick_value(M, i, j, k + 1);
+            q[2] = brick_value(M, i, j + 1, k), q[3] = brick_value(M, i, j + 1, k + 1);
+            q[4] = brick_value(M, i + 1, j, k), q[5] = brick_value(M, i + 1, j, k + 1);
+            q[6] = brick_value(M, i + 1, j + 1, k), q[7] = brick_value(M, i + 1, j + 1, k + 1);
         }
-    } else if (i >= 0 && j >= 0 && k >= 0 && i + 1 < M.nx && j + 1 < M.ny && k + 1 < M.nz) {
-        // interior cell: the x-neighbours are adjacent words, four dword-aligned dwordx2 loads
-        typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
-        using g2 = __attribute__((address_space(1))) const f2u;
-        const float* b = M.density + ((size_t)k * M.ny + (size_t)j) * M.nx + (size_t)i;
-        const size_t sy = (size_t)M.nx, sz = (size_t)M.nx * M.ny;
-        const f2u a = *(g2*)b, c = *(g2*)(b + sz), e = *(g2*)(b + sy), f = *(g2*)(b + sy + sz);
-        d000 = a.x, d100 = a.y, d001 = c.x, d101 = c.y, d010 = e.x, d110 = e.y, d011 = f.x, d111 = f.y;
+    } else if (dense_interior(M, C)) {
+        dense_corners(M, C, q);
     } else {
-        d000 = grid_value(M, i, j, k), d001 = grid_value(M, i, j, k + 1);
-        d010 = grid_value(M, i, j + 1, k), d011 = grid_value(M, i, j + 1, k + 1);
-        d100 = grid_value(M, i + 1, j, k), d101 = grid_value(M, i + 1, j, k + 1);
-        d110 = grid_value(M, i + 1, j + 1, k), d111 = grid_value(M, i + 1, j + 1, k + 1);
+        q[0] = grid_value(M, i, j, k), q[1] = grid_value(M, i, j, k + 1);
+        q[2] = grid_value(M, i, j + 1, k), q[3] = grid_value(M, i, j + 1, k + 1);
+        q[4] = grid_value(M, i + 1, j, k), q[5] = grid_value(M, i + 1, j, k + 1);
+        q[6] = grid_value(M, i + 1, j + 1, k), q[7] = grid_value(M, i + 1, j + 1, k + 1);
     }
-    const float g = vdb_lerp(vdb_lerp(vdb_lerp(d000, d001, w), vdb_lerp(d010, d011, w), v),
-                             vdb_lerp(vdb_lerp(d100, d101, w), vdb_lerp(d110, d111, w), v), u);
-    return M.multiplier * g;   // HeterogeneousMedium::getDensity (Src/medium.cpp:24-27)
+    return vdb_interp(M, C, q);
 }
 
 // Medium::sampleWavelength + DiscreteEmpiricalDistribution1D (Src/medium.h:102-115,
@@ -791,7 +814,8 @@ __device__ int delta_track(const KParams& P, v3 o, v3 d, v3 thr, float& t, float
             pos = ray_at(o, d, t1 + kRAY_EPS);
             dir = d;
             const float dist = s - (t - (t1 - kRAY_EPS));
-            const v3 tr = vexp((-vmaj) * dist);
+            const float e = glibc_expf(-majorant * dist);   // vexp((-vmaj) * dist)
+            const v3 tr = mk(e, e, e);
             const v3 pdf = pmf * tr;
             tt = tt * (tr / (pdf.x + pdf.y + pdf.z));
             tm = isnan3(tt) ? mk(0, 0, 0) : tt;
@@ -801,18 +825,23 @@ __device__ int delta_track(const KParams& P, v3 o, v3 d, v3 thr, float& t, float
         const v3 sigma_s = scatter * density;
         sa = absorb * density;
         const v3 sigma_n = (vmaj - sa) - sigma_s;
-        const v3 P_s = sigma_s / (sigma_s + sigma_n);
-        const v3 P_n = sigma_n / (sigma_s + sigma_n);
-        if (rng.next() < comp(P_s, channel)) {
+        const v3 den = sigma_s + sigma_n;
+        // P_s = sigma_s / (sigma_s + sigma_n): the acceptance test reads one component, the
+        // scattering branch all three (the same quotients, computed where they are used)
+        if (rng.next() < comp(sigma_s, channel) / comp(den, channel)) {
+            const v3 P_s = sigma_s / den;
             pos = ray_at(o, d, t);
             hg_sample(M.g, d, rng, dir);
-            const v3 tr = vexp((-vmaj) * s);
+            const float e = glibc_expf(-majorant * s);   // vexp((-vmaj) * s): three equal arguments
+            const v3 tr = mk(e, e, e);
             const v3 pdf = (pmf * (tr * majorant)) * P_s;
             tt = tt * ((tr * sigma_s) / (pdf.x + pdf.y + pdf.z));
             tm = isnan3(tt) ? mk(0, 0, 0) : tt;
             return 1;
         }
-        const v3 tr = vexp((-vmaj) * s);
+        const v3 P_n = sigma_n / den;
+        const float e = glibc_expf(-majorant * s);
+        const v3 tr = mk(e, e, e);
         const v3 pdf = (pmf * (tr * majorant)) * P_n;
         tt = tt * ((tr * sigma_n) / (pdf.x + pdf.y + pdf.z));
     }
@@ -1559,8 +1588,11 @@ __device__ int nee_resume(const KParams& P, uint32_t s, v3 thr_m, v3& rad, Rng& 
 #ifndef XRT_STEP_WAVES
 #define XRT_STEP_WAVES 4   // min waves per SIMD the compiler must fit k_step into (<= 128 VGPRs)
 #endif
+#ifndef XRT_KSTEP_WAVES
+#define XRT_KSTEP_WAVES XRT_STEP_WAVES
+#endif
 template <int SCN, int INTEG>
-__global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step(KParams P, const uint32_t* __restrict__ list,
+__global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, const uint32_t* __restrict__ list,
                                                   const uint32_t* __restrict__ count, uint32_t* __restrict__ out,
                                                   uint32_t* out_count, uint32_t* zero_count, uint32_t* req_count,
                                                   uint32_t visits) {
