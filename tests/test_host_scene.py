@@ -103,3 +103,49 @@ def test_obj_parser_negative_indices_and_vn(tmp_path):
     assert d.objects[names.index("tri2")].material == abi.XRT_MAT_NONE   # no_surface -> nullptr
     tn = np.ctypeslib.as_array(d.tri_n, shape=(d.n_tris * 9,)).reshape(-1, 3, 3)
     assert np.array_equal(tn[a.first, 0], [0, 0, 1])
+
+
+def _polygon_obj(tmp_path, polys):
+    """An OBJ with one shape per polygon (vertex lists in the z = 1 plane) and one material."""
+    (tmp_path / "p.mtl").write_text("newmtl white\nKd 0.5 0.5 0.5\n")
+    lines, base = ["mtllib p.mtl"], 1
+    for name, pts in polys:
+        lines.append(f"o {name}")
+        lines += [f"v {x} {y} 1.0" for x, y in pts]
+        lines.append("usemtl white")
+        lines.append("f " + " ".join(str(base + k) for k in range(len(pts))))
+        base += len(pts)
+    path = tmp_path / "p.obj"
+    path.write_text("\n".join(lines) + "\n")
+    return str(path)
+
+
+def _area2(t):
+    (ax, ay), (bx, by), (cx, cy) = t[:, :2].astype(np.float64)
+    return (bx - ax) * (cy - ay) - (by - ay) * (cx - ax)
+
+
+@pytest.mark.parametrize("name,pts", [
+    ("hexagon", [(2, 0), (1, 1.7), (-1, 1.7), (-2, 0), (-1, -1.7), (1, -1.7)]),
+    ("arrow", [(0, 0), (4, 0), (4, 3), (2, 1), (0, 3)]),              # concave: reflex corner at (2, 1)
+    ("comb", [(0, 0), (6, 0), (6, 4), (5, 4), (5, 1), (3, 1), (3, 4), (2, 4), (2, 1), (0, 1)]),
+])
+def test_tinyobj_ear_clipping_polygons(tmp_path, name, pts):
+    """Faces of five or more vertices go through tinyobjloader's built-in ear clipping
+    (Src/scene.cpp:54 ParseFromFile with triangulate = true).  tinyobjloader is absent, so the
+    exact triangle list is parity-unpinned; what ear clipping guarantees is checked: n - 2
+    triangles, none wound against the polygon (collinear vertices may give a zero-area one,
+    as tinyobjloader's test `cross * area < 0` lets through), covering exactly the
+    polygon's area, using only the polygon's vertices."""
+    s = scenes.SceneBundle()
+    s.load_obj(_polygon_obj(tmp_path, [(name, pts)]))
+    s.flatten()
+    tris = s.triangles()
+    assert len(tris) == len(pts) - 2
+    p = np.array(pts, np.float64)
+    poly2 = np.sum(p[:, 0] * np.roll(p[:, 1], -1) - np.roll(p[:, 0], -1) * p[:, 1])
+    areas = [_area2(t) for t in tris]
+    assert all(a * poly2 >= 0 for a in areas)
+    assert abs(sum(areas) - poly2) < 1e-3
+    verts = {tuple(np.float32(v)) for v in np.array([(x, y, 1.0) for x, y in pts], np.float32)}
+    assert all(tuple(v) in verts for t in tris for v in t)

@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <limits>
 #include <map>
 #include <sstream>
 
@@ -205,9 +206,11 @@ bool Image::writePPM(const std::string& filename) const {  // Src/image.h:92-114
 // A restatement of the parts of tinyobjloader v2 (2.0.0rc13, the vcpkg port current at the
 // reference snapshot; third-party, absent here) that Scene::loadObj relies on:
 // tryParseDouble number parsing, 1-based/negative index fixing, shapes split at `o`/`g`,
-// faces flushed at `usemtl` changes, quads split along the shorter diagonal, MTL Kd/Ke/
-// illum/unknown parameters.  Polygons with more than four vertices are fan-triangulated
-// (tinyobjloader uses ear clipping there; none of the testdata has such faces).
+// faces flushed at `usemtl` changes, quads split along the shorter diagonal, polygons of five
+// or more vertices by tinyobjloader's built-in ear clipping (tinyobj_ear_clip below), MTL
+// Kd/Ke/illum/unknown parameters.  Parity of the ear clipping is unpinned: the library is
+// absent and no reference test or testdata file has such a face (tests/test_host_scene.py
+// checks its invariants: n - 2 triangles covering the polygon).
 namespace {
 
 bool tinyobj_parse_double(const char* s, const char* end, double* result) {
@@ -345,6 +348,85 @@ bool load_mtl(const std::string& path, std::vector<ObjMaterial>& mats, std::map<
     return true;
 }
 
+// tinyobjloader's pnpoly: even-odd crossing test of (tx, ty) against the triangle (vx, vy)
+int tinyobj_pnpoly(const float* vx, const float* vy, float tx, float ty) {
+    int c = 0;
+    for (int i = 0, j = 2; i < 3; j = i++)
+        if (((vy[i] > ty) != (vy[j] > ty)) && (tx < (vx[j] - vx[i]) * (ty - vy[i]) / (vy[j] - vy[i]) + vx[i])) c = !c;
+    return c;
+}
+
+// exportGroupsToShape's built-in ear clipping (tinyobjloader v2, no TINYOBJLOADER_USE_MAPBOX_
+// EARCUT, real_t = float): project on the two axes that drop the largest component of the
+// first corner's cross product; walk `guess` around the remaining polygon, emit the
+// triangle (guess, guess + 1, guess + 2) unless it turns against the polygon's running
+// "area" sign (an inner corner) or another remaining vertex lies in it, then remove vertex
+// guess + 1; give up after a full lap without an ear; the last three vertices are the last
+// triangle.  Appends the triangles (index triples) to `out`.
+void tinyobj_ear_clip(const std::vector<VRef>& face, const std::vector<float>& v, std::vector<VRef>& out) {
+    const size_t n0 = face.size();
+    size_t axes[2] = {1, 2};
+    for (size_t k = 0; k < n0; ++k) {
+        const size_t a = (size_t)face[k % n0].v, b = (size_t)face[(k + 1) % n0].v, c = (size_t)face[(k + 2) % n0].v;
+        if (3 * a + 2 >= v.size() || 3 * b + 2 >= v.size() || 3 * c + 2 >= v.size()) continue;
+        const float e0x = v[3 * b] - v[3 * a], e0y = v[3 * b + 1] - v[3 * a + 1], e0z = v[3 * b + 2] - v[3 * a + 2];
+        const float e1x = v[3 * c] - v[3 * b], e1y = v[3 * c + 1] - v[3 * b + 1], e1z = v[3 * c + 2] - v[3 * b + 2];
+        const float cx = std::fabs(e0y * e1z - e0z * e1y), cy = std::fabs(e0z * e1x - e0x * e1z),
+                    cz = std::fabs(e0x * e1y - e0y * e1x);
+        const float eps = std::numeric_limits<float>::epsilon();
+        if (cx > eps || cy > eps || cz > eps) {
+            if (!(cx > cy && cx > cz)) {
+                axes[0] = 0;
+                if (cz > cx && cz > cy) axes[1] = 1;
+            }
+            break;
+        }
+    }
+    std::vector<VRef> rem = face;
+    size_t guess = 0, iters = n0, prev = rem.size();
+    VRef ind[3];
+    float vx[3], vy[3];
+    while (rem.size() > 3 && iters > 0) {
+        const size_t np = rem.size();
+        if (guess >= np) guess -= np;
+        if (prev != np) prev = np, iters = np;
+        else --iters;
+        for (int k = 0; k < 3; ++k) {
+            ind[k] = rem[(guess + k) % np];
+            const size_t vi = (size_t)ind[k].v;
+            const bool bad = vi * 3 + axes[0] >= v.size() || vi * 3 + axes[1] >= v.size();
+            vx[k] = bad ? 0.0f : v[vi * 3 + axes[0]];
+            vy[k] = bad ? 0.0f : v[vi * 3 + axes[1]];
+        }
+        const float e0x = vx[1] - vx[0], e0y = vy[1] - vy[0], e1x = vx[2] - vx[1], e1y = vy[2] - vy[1];
+        const float cross = e0x * e1y - e0y * e1x;
+        const float area = (vx[0] * vy[1] - vy[0] * vx[1]) * 0.5f;
+        if (cross * area < 0.0f) {   // an inner corner
+            guess += 1;
+            continue;
+        }
+        bool overlap = false;
+        for (size_t other = 3; other < np; ++other) {
+            const size_t idx = (guess + other) % np;
+            const size_t ovi = (size_t)rem[idx].v;
+            if (ovi * 3 + axes[0] >= v.size() || ovi * 3 + axes[1] >= v.size()) continue;
+            if (tinyobj_pnpoly(vx, vy, v[ovi * 3 + axes[0]], v[ovi * 3 + axes[1]])) {
+                overlap = true;
+                break;
+            }
+        }
+        if (overlap) {
+            guess += 1;
+            continue;
+        }
+        for (int k = 0; k < 3; ++k) out.push_back(ind[k]);   // an ear
+        for (size_t r = (guess + 1) % np; r + 1 < np; ++r) rem[r] = rem[r + 1];
+        rem.pop_back();
+    }
+    if (rem.size() == 3)
+        for (int k = 0; k < 3; ++k) out.push_back(rem[k]);
+}
+
 int fix_index(int idx, int n, bool& ok) {
     if (idx > 0) return idx - 1;
     if (idx == 0) { ok = false; return 0; }
@@ -386,13 +468,13 @@ bool Scene::loadObj(const std::string& filepath) {
                     for (int c = 0; c < 3; ++c) cur.idx.push_back(fc[t[k][c]]);
                     cur.material.push_back(material);
                 }
+            } else if (n == 3) {
+                for (int c = 0; c < 3; ++c) cur.idx.push_back(fc[c]);
+                cur.material.push_back(material);
             } else {
-                for (size_t k = 1; k + 1 < n; ++k) {
-                    cur.idx.push_back(fc[0]);
-                    cur.idx.push_back(fc[k]);
-                    cur.idx.push_back(fc[k + 1]);
-                    cur.material.push_back(material);
-                }
+                const size_t before = cur.idx.size();
+                tinyobj_ear_clip(fc, pos, cur.idx);
+                for (size_t k = before; k < cur.idx.size(); k += 3) cur.material.push_back(material);
             }
         }
         faces.clear();
