@@ -50,6 +50,19 @@ struct SkipNode {
 };
 std::vector<SkipNode> thread_bvh(const BvhBuild& b);
 
+// 4-wide form of a BvhBuild (two-level trace, k_trace_deep_pt): each binary node absorbs
+// its interior children (largest box first) until it has four children, so a traversal
+// step fetches four child boxes (128 bytes) and the tree is about half as deep.  Child c:
+// bmin[c], bmax[c]; count[c] > 0: a leaf of count[c] primitives from index[c] (the same
+// reordered primitive array), 0: the interior node index[c], -1: empty.  Stored as 8 float4
+// {bmin, index} x 4, {bmax, count} x 4; the first kBvhTopNodes (breadth-first) come first.
+struct Bvh4Node {
+    float lo[4][4];   // bmin xyz, index (int bits)
+    float hi[4][4];   // bmax xyz, count (int bits)
+};
+// `depth`: the deepest node (a traversal pushes at most 3 children per level)
+std::vector<Bvh4Node> collapse_bvh4(const BvhBuild& b, int& depth);
+
 // prim_min / prim_max: n boxes (3 floats each).  Binned SAH, leaves of <= leaf_max
 // primitives, median split below max_depth - 8 levels of headroom; margin pads every box.
 BvhBuild build_bvh(const float* prim_min, const float* prim_max, uint32_t n, uint32_t leaf_max, float margin,

@@ -199,4 +199,63 @@ std::vector<SkipNode> thread_bvh(const BvhBuild& b) {
     return out;
 }
 
+namespace {
+struct Child {
+    const float* mn;
+    const float* mx;
+    int32_t index, count;
+};
+float child_area(const Child& c) {
+    const float dx = c.mx[0] - c.mn[0], dy = c.mx[1] - c.mn[1], dz = c.mx[2] - c.mn[2];
+    return 2.0f * (dx * dy + dy * dz + dz * dx);
+}
+}  // namespace
+
+std::vector<Bvh4Node> collapse_bvh4(const BvhBuild& b, int& depth) {
+    std::vector<Bvh4Node> out;
+    depth = 0;
+    if (b.nodes.empty()) return out;
+    // breadth-first over binary interior nodes that become 4-wide nodes
+    std::vector<std::pair<uint32_t, int>> queue{{0u, 0}};   // (binary node, depth)
+    std::vector<std::vector<Child>> kids;
+    for (size_t head = 0; head < queue.size(); ++head) {
+        const BvhNode& n = b.nodes[queue[head].first];
+        std::vector<Child> ch;
+        if (n.lcount >= 0) ch.push_back(Child{n.lmin, n.lmax, n.left, n.lcount});
+        if (n.rcount >= 0) ch.push_back(Child{n.rmin, n.rmax, n.right, n.rcount});
+        while (ch.size() < 4) {   // open the interior child with the largest box
+            int best = -1;
+            for (size_t c = 0; c < ch.size(); ++c)
+                if (ch[c].count == 0 && (best < 0 || child_area(ch[c]) > child_area(ch[(size_t)best]))) best = (int)c;
+            if (best < 0) break;
+            const BvhNode& m = b.nodes[(size_t)ch[(size_t)best].index];
+            ch.erase(ch.begin() + best);
+            if (m.lcount >= 0) ch.push_back(Child{m.lmin, m.lmax, m.left, m.lcount});
+            if (m.rcount >= 0) ch.push_back(Child{m.rmin, m.rmax, m.right, m.rcount});
+        }
+        depth = std::max(depth, queue[head].second);
+        for (Child& c : ch)
+            if (c.count == 0) {   // becomes the 4-wide node numbered queue.size()
+                queue.push_back({(uint32_t)c.index, queue[head].second + 1});
+                c.index = (int32_t)(queue.size() - 1);
+            }
+        kids.push_back(std::move(ch));
+    }
+    out.resize(kids.size());
+    for (size_t i = 0; i < kids.size(); ++i) {
+        Bvh4Node& nd = out[i];
+        for (int c = 0; c < 4; ++c) {
+            const bool has = (size_t)c < kids[i].size();
+            int32_t index = has ? kids[i][(size_t)c].index : 0, count = has ? kids[i][(size_t)c].count : -1;
+            for (int q = 0; q < 3; ++q) {
+                nd.lo[c][q] = has ? kids[i][(size_t)c].mn[q] : FLT_MAX;
+                nd.hi[c][q] = has ? kids[i][(size_t)c].mx[q] : -FLT_MAX;
+            }
+            std::memcpy(&nd.lo[c][3], &index, 4);
+            std::memcpy(&nd.hi[c][3], &count, 4);
+        }
+    }
+    return out;
+}
+
 }  // namespace xrt

@@ -437,66 +437,72 @@ __global__ __launch_bounds__(kBlock) void k_trace_2a(KParams P, const uint32_t* 
     }
 }
 
-template <int NL, typename SE>
-__global__ __launch_bounds__(kBlock) void k_trace_deep(KParams P) {
-    extern __shared__ uint32_t bvh_stack_lds[];
-    const int tid = threadIdx.x;
-    const int ntop = P.bvh_nodes < (int)kBvhTopNodes ? P.bvh_nodes : (int)kBvhTopNodes;
-    f4* top = reinterpret_cast<f4*>(bvh_stack_lds);
-    for (int q = tid; q < 4 * ntop; q += kBlock) top[q] = P.bvh_node[q];
-    SE* stack = reinterpret_cast<SE*>(bvh_stack_lds + 16 * ntop);
-    __syncthreads();
-    const PartIter it = part_iter(P, P.deep_count, kBlock);
-    const uint32_t* dq = P.deep + (size_t)it.p * P.deep_cap;
-    SE* stk = stack + tid;
-    for (uint32_t base = it.first; base < it.n; base += it.stride) {
-        const uint32_t i = base + tid;
-        if (i >= it.n) continue;
-        const uint32_t e = dq[i], s = e >> 3, kind = e & 7u;
-        if (kind == 0) {
-            const f4 h = P.hit[s];
-            float bt = h.x, bu = h.y, bv = h.z;
-            int bk = __float_as_int(h.w);
-            (void)bvh_trace<false, SE>(P, top, ntop, stk, xyz(P.ray_o[s]), xyz(P.ray_d[s]), kINF, bt, bu, bv, bk);
-            P.hit[s] = make_float4(bt, bu, bv, __int_as_float(bk));
+// bvh_leaf for a leaf of at most kBvhLeaf triangles with every triangle's loads issued before
+// the first test (one memory round trip per leaf instead of one per triangle); tests and
+// updates in the same order as bvh_leaf.
+template <bool ANY>
+__device__ __forceinline__ bool bvh_leaf_batch(const KParams& P, int first, int count, v3 o, v3 d, float tmax,
+                                               float& bt, float& bu, float& bv, int& bk) {
+    f4 T[kBvhLeaf][3];
+#pragma unroll
+    for (int q = 0; q < (int)kBvhLeaf; ++q)
+        if (q < count) T[q][0] = P.bvh_tri[3 * (first + q)], T[q][1] = P.bvh_tri[3 * (first + q) + 1],
+                       T[q][2] = P.bvh_tri[3 * (first + q) + 2];
+#pragma unroll
+    for (int q = 0; q < (int)kBvhLeaf; ++q) {
+        if (q >= count) break;
+        if (ANY && T[q][1].w == 0.0f) continue;   // area-light objects never occlude
+        float t, u, v;
+        if (!ray_tri(o, d, xyz(T[q][0]), xyz(T[q][1]), xyz(T[q][2]), t, u, v)) continue;
+        if (ANY) {
+            if (t < tmax) return true;
         } else {
-            const uint32_t l = kind - 1u;
-            const f4 a = P.sh_o[(size_t)l * P.n_slots + s];
-            float bt = kINF, bu, bv;
-            int bk = -1;
-            if (bvh_trace<true, SE>(P, top, ntop, stk, xyz(a), xyz(P.sh_d[(size_t)l * P.n_slots + s]), a.w, bt, bu, bv, bk))
-                atomicOr(P.occ + s, 1u << l);
+            const int k = __float_as_int(T[q][2].w);
+            if (t < bt || (t == bt && k < bk)) bt = t, bu = u, bv = v, bk = k;
         }
     }
+    return false;
 }
 
-// Phase B with dynamic ray fetch.  In k_trace_deep a wave holds its 64 rays until the
-// longest traversal ends (measured lane utilisation 0.095: most queued rays cross the mesh's
-// box and leave after a few nodes, a few descend to the surface).  Here a lane whose ray is
-// done takes the next queued ray of its partition (one atomic per wave per refill, when at
-// least 16 lanes are idle or the wave is empty), so lanes stay busy until the queue drains.
-// One loop iteration = one node of each active lane's traversal (bvh_trace's step: both
-// children tested, leaves first, nearer interior child next, farther one stacked); closest
-// hits keep bvh_leaf's (t, index) order, any-hit rays stop at the first occluder.
+// Phase B: the queued rays walk the BVH's 4-wide form (bvh.h Bvh4Node: a step fetches four
+// child boxes, the tree is about half as deep as the binary one), with dynamic ray fetch —
+// a lane whose ray is done takes the next queued ray of its partition (one atomic per wave
+// per refill, when at least 16 lanes are idle or the wave is empty), so lanes stay busy
+// until the queue drains (a static assignment measured lane utilisation 0.095: most queued
+// rays cross the mesh's box and leave after a few nodes, a few descend to the surface).
+// One loop iteration = one node per active lane: the four children tested against [0, lim]
+// (lim = best t, inclusive, for closest hits; tmax for shadow rays), leaf children first
+// (bvh_leaf: the (t, index) order; shadow rays stop at the first occluder), then the nearest
+// interior child that still overlaps [0, best t] is next and the other overlapping ones are
+// stacked.  Exact for the same reason as bvh_trace: every triangle whose padded box overlaps
+// [0, best t] is tested, whatever the order.
 template <typename SE>
-__global__ __launch_bounds__(kBlock) void k_trace_deep_pt(KParams P) {
+__global__ __launch_bounds__(kBlock) void k_trace_deep4(KParams P) {
     extern __shared__ uint32_t bvh_stack_lds[];
     const int tid = threadIdx.x, lane = tid & 63;
-    const int ntop = P.bvh_nodes < (int)kBvhTopNodes ? P.bvh_nodes : (int)kBvhTopNodes;
+    const int ntop = P.bvh4_nodes < (int)kBvhTopNodes ? P.bvh4_nodes : (int)kBvhTopNodes;
     f4* top = reinterpret_cast<f4*>(bvh_stack_lds);
-    for (int q = tid; q < 4 * ntop; q += kBlock) top[q] = P.bvh_node[q];
-    SE* stk = reinterpret_cast<SE*>(bvh_stack_lds + 16 * ntop) + tid;
+    for (int q = tid; q < 8 * ntop; q += kBlock) top[q] = P.bvh4[q];
+    SE* stk = reinterpret_cast<SE*>(bvh_stack_lds + 32 * ntop) + tid;
     __syncthreads();
     const uint32_t p = blockIdx.x % P.n_part;
     const uint32_t cnt = P.deep_count[p];
     uint32_t* next_ctr = P.deep_count + kMaxParts + p;
     const uint32_t* dq = P.deep + (size_t)p * P.deep_cap;
+#ifdef XRT_EXPERIMENTS
+    if (blockIdx.x < P.n_part && tid == 0) atomicAdd(P.stats + 38, (unsigned long long)cnt);
+    uint32_t nsteps = 0, niter = 0;
+#endif
     bool active = false, drained = cnt == 0, any = false;
     uint32_t s = 0, l = 0;
     int node = 0, sp = 0, bk = -1;
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0), inv = mk(0, 0, 0);
     float tmax = 0.0f, bt = kINF, bu = 0.0f, bv = 0.0f;
     while (true) {
+#ifdef XRT_EXPERIMENTS
+        nsteps += active ? 1u : 0u;
+        ++niter;
+#endif
         const uint64_t idle = __ballot(!active);
         const uint32_t nidle = (uint32_t)__popcll(idle);
         if (!drained && (nidle >= 16u || nidle == 64u)) {
@@ -532,41 +538,44 @@ __global__ __launch_bounds__(kBlock) void k_trace_deep_pt(KParams P) {
         }
         if (!__ballot(active)) break;
         if (!active) continue;
-        f4 n0, n1, n2, n3;
-        if (node < ntop) {
-            const f4* N = top + 4 * node;
-            n0 = N[0], n1 = N[1], n2 = N[2], n3 = N[3];
-        } else {
-            const f4* N = P.bvh_node + 4 * (size_t)node;
-            n0 = N[0], n1 = N[1], n2 = N[2], n3 = N[3];
+        f4 lo[4], hi[4];
+        {
+            const f4* N = node < ntop ? top + 8 * node : P.bvh4 + 8 * (size_t)node;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) lo[c] = N[c], hi[c] = N[4 + c];
         }
-        const float lim = any ? tmax : bt;
-        const int lcount = __float_as_int(n1.w), rcount = __float_as_int(n3.w);
-        const float el = lcount >= 0 ? bvh_enter(n0, n1, o, inv, lim) : __builtin_inff();
-        const float er = rcount >= 0 ? bvh_enter(n2, n3, o, inv, lim) : __builtin_inff();
-        const bool hl = el != __builtin_inff(), hr = er != __builtin_inff();
+        float e[4];
+        {
+            const float lim = any ? tmax : bt;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                e[c] = __float_as_int(hi[c].w) >= 0 ? bvh_enter(lo[c], hi[c], o, inv, lim) : __builtin_inff();
+        }
         bool occluded = false;
-        // leaves first (either order gives the same result)
-        if (hl && lcount > 0) {
-            occluded = any ? bvh_leaf<true>(P, __float_as_int(n0.w), lcount, o, d, tmax, bt, bu, bv, bk)
-                           : bvh_leaf<false>(P, __float_as_int(n0.w), lcount, o, d, tmax, bt, bu, bv, bk);
-        }
-        if (!occluded && hr && rcount > 0) {
-            occluded = any ? bvh_leaf<true>(P, __float_as_int(n2.w), rcount, o, d, tmax, bt, bu, bv, bk)
-                           : bvh_leaf<false>(P, __float_as_int(n2.w), rcount, o, d, tmax, bt, bu, bv, bk);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {   // leaves first (either order gives the same result)
+            const int k = __float_as_int(hi[c].w);
+            if (!occluded && k > 0 && e[c] != __builtin_inff())
+                occluded = any ? bvh_leaf_batch<true>(P, __float_as_int(lo[c].w), k, o, d, tmax, bt, bu, bv, bk)
+                               : bvh_leaf_batch<false>(P, __float_as_int(lo[c].w), k, o, d, tmax, bt, bu, bv, bk);
         }
         bool done = occluded;
         if (!done) {
-            const bool il = hl && lcount == 0, ir = hr && rcount == 0;
+            // interior children still overlapping [0, lim] (bt may have shrunk at the leaves:
+            // e <= bt is the same test as a fresh one against the smaller limit)
+            const float lim = any ? tmax : bt;
             int nx = -1;
-            if (il && ir) {
-                const bool lfirst = any || el <= er;
-                nx = __float_as_int(lfirst ? n0.w : n2.w);
-                stk[(sp++) * kBlock] = (SE)__float_as_int(lfirst ? n2.w : n0.w);
-            } else if (il) {
-                nx = __float_as_int(n0.w);
-            } else if (ir) {
-                nx = __float_as_int(n2.w);
+            float en = __builtin_inff();
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                if (__float_as_int(hi[c].w) != 0 || !(e[c] <= lim)) continue;
+                const int idx = __float_as_int(lo[c].w);
+                if (nx < 0 || e[c] < en) {
+                    if (nx >= 0) stk[(sp++) * kBlock] = (SE)nx;
+                    nx = idx, en = e[c];
+                } else {
+                    stk[(sp++) * kBlock] = (SE)idx;
+                }
             }
             if (nx >= 0) node = nx;
             else if (sp == 0) done = true;
@@ -578,6 +587,10 @@ __global__ __launch_bounds__(kBlock) void k_trace_deep_pt(KParams P) {
             active = false;
         }
     }
+#ifdef XRT_EXPERIMENTS
+    atomicAdd(P.stats + 39, (unsigned long long)nsteps);
+    if (lane == 0) atomicAdd(P.stats + 37, (unsigned long long)niter), atomicMax(P.stats + 36, (unsigned long long)niter);
+#endif
 }
 
 // Small triangle scenes (<= kSmallTris triangles, e.g. the Cornell box): every triangle
@@ -2461,10 +2474,15 @@ hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* 
             if (e == hipSuccess) e = hipGetLastError();
             if (e != hipSuccess) return e;
             // persistent: up to 2048 blocks (8 per CU), each serving partition blockIdx % n_part
+            if (!P.bvh4 || P.bvh4_stack <= 0 || P.bvh4_stack > kBvh4Stack) return hipErrorInvalidValue;
             const uint32_t db = P.n_part * std::max<uint32_t>(1u, std::min<uint32_t>(2048u / P.n_part,
                                                                                     (P.deep_cap + kBlock - 1) / kBlock));
-            if (small) hipLaunchKernelGGL((k_trace_deep_pt<uint16_t>), dim3(db), dim3(kBlock), lds, st, P);
-            else hipLaunchKernelGGL((k_trace_deep_pt<uint32_t>), dim3(db), dim3(kBlock), lds, st, P);
+            const bool small4 = P.bvh4_nodes <= 0x10000;
+            const size_t ntop4 = std::min<size_t>((size_t)P.bvh4_nodes, kBvhTopNodes);
+            const size_t lds4 = ntop4 * 8 * sizeof(f4) +
+                                (size_t)P.bvh4_stack * kBlock * (small4 ? sizeof(uint16_t) : sizeof(uint32_t));
+            if (small4) hipLaunchKernelGGL((k_trace_deep4<uint16_t>), dim3(db), dim3(kBlock), lds4, st, P);
+            else hipLaunchKernelGGL((k_trace_deep4<uint32_t>), dim3(db), dim3(kBlock), lds4, st, P);
             return hipGetLastError();
         }
         if (small && nl1)

@@ -41,7 +41,7 @@ struct xrt_ctx {
     // scene
     std::vector<DevBuf*> scene_bufs;
     DevBuf tri, tri_ng, tri_nrm, sph, sph_obj, box, objs, lights, segs, density, obj_box, obj_plane, bvh_node,
-        bvh_tri, snode, ssph, sbk, stri, sbox, splane;
+        bvh_tri, snode, ssph, sbk, stri, sbox, splane, bvh4;
     KParams base{};
     StepObjs step_objs{};   // kernel-argument object records of the merged-trace schedule
     StepObjs sstep{};       // two-level trace: the small objects' records (KParams::sstep)
@@ -226,7 +226,7 @@ void xrt_destroy(xrt_ctx* c) {
                      &c->sample_k, &c->depth, &c->occ, &c->rng_c, &c->rng_g, &c->ring, &c->c_seg, &c->c_shadow,
                      &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch, &c->kparams};
     for (DevBuf* b : all) free_buf(*b);
-    free_buf(c->stri), free_buf(c->sbox), free_buf(c->splane), free_buf(c->deep);
+    free_buf(c->stri), free_buf(c->sbox), free_buf(c->splane), free_buf(c->bvh4), free_buf(c->deep);
     free_buf(c->stage), free_buf(c->q_rays), free_buf(c->q_tmax), free_buf(c->q_out);
     free_buf(c->brick_table), free_buf(c->brick_data);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
@@ -412,7 +412,7 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
     // hit position, so box tests never drop a hit the linear scan accepts.
     P.bvh_node = nullptr, P.bvh_tri = nullptr, P.bvh_stack = 0, P.bvh_nodes = 0;
     P.stri = nullptr, P.sbox = nullptr, P.splane = nullptr, P.n_stri = 0, P.n_sobj = 0, P.two_level = 0;
-    P.sstep = nullptr;
+    P.sstep = nullptr, P.bvh4 = nullptr, P.bvh4_nodes = 0, P.bvh4_stack = 0;
     if (P.scene_kind == SCN_TRI && !P.small_tri && P.n_tris > 0 && !exp_env("XRT_NO_BVH")) {
         // two-level split: mesh objects of more than kLargeObjTris triangles go into the BVH,
         // the rest (if any, and if they fit the LDS scan) are scanned directly
@@ -502,6 +502,13 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
         P.bvh_node = as<f4>(c->bvh_node), P.bvh_tri = as<f4>(c->bvh_tri);
         P.bvh_stack = B.depth + 1;
         P.bvh_nodes = (int)B.nodes.size();
+        if (P.two_level) {   // the deep rays walk the 4-wide form
+            int d4 = 0;
+            const std::vector<Bvh4Node> b4 = collapse_bvh4(B, d4);
+            if (3 * d4 + 1 > kBvh4Stack) return set_err(c, XRT_ERR_UNSUPPORTED, "4-wide BVH deeper than the traversal stack");
+            if ((rc = upload(c, c->bvh4, b4.data(), b4.size() * sizeof(Bvh4Node)))) return rc;
+            P.bvh4 = as<f4>(c->bvh4), P.bvh4_nodes = (int)b4.size(), P.bvh4_stack = 3 * d4 + 1;
+        }
     }
     // sphere scenes (C3's 1001 spheres): a threaded BVH for the fused schedule's traces.
     // Sphere boxes: center +- radius, padded by 1e-4 of the scene diagonal + 1e-4 —
@@ -911,6 +918,9 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     unsigned long long hs[40] = {0};
     HIPCHK(c, hipMemcpy(hs, P.stats, 40 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     if (hs[5] || hs[6]) std::fprintf(stderr, "[xrt] triangle tests: lane %llu wave %llu\n", hs[5], hs[6]);
+    if (hs[38])   // experiment builds
+        std::fprintf(stderr, "[xrt] deep rays %llu node steps %llu wave iterations %llu max wave iterations %llu\n",
+                     hs[38], hs[39], hs[37], hs[36]);
     if (hs[8] || hs[9]) {   // -DXRT_PHASE_CLOCK experiment builds
         std::fprintf(stderr, "[xrt] phase cycles (sum over waves):");
         for (int q = 8; q < 16; ++q) std::fprintf(stderr, " %llu", hs[q]);
