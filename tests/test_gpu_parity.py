@@ -271,7 +271,7 @@ def test_merged_segments_per_launch(renderer, visits):
         assert (g.segments, g.shadow_rays, g.draws) == (st["segments"], st["shadow_rays"], st["draws"])
 
 
-@pytest.mark.parametrize("spw,group", [(16, True), (32, True), (64, True), (16, False), (32, False)])
+@pytest.mark.parametrize("spw,group", [(4, True), (16, True), (32, True), (64, True), (16, False), (32, False)])
 def test_merged_slots_per_wave(renderer, spw, group):
     """The merged kernel's layouts for small pixel shards — 16 or 32 slots per wave, their
     traces shared by 4 or 2 lanes per slot (group trace) or spread over idle lanes

@@ -265,7 +265,7 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
     occ = W.occ[lane];
 }
 
-// Group trace (G = 2 or 4 lanes per slot, scenes of <= 64 triangles): the G lanes of a
+// Group trace (G = 2, 4 or 16 lanes per slot, scenes of <= 64 triangles): the G lanes of a
 // slot hold identical path state (every shading instruction runs on all of them) and split
 // its traces among themselves, with no LDS traffic but the triangle fetches: lane u culls
 // objects u, u+G, ... into 64-bit triangle masks (one per ray), the masks are OR-ed across
@@ -278,8 +278,10 @@ __device__ __forceinline__ uint32_t dpp32(uint32_t x) {
 }
 template <int G>
 __device__ __forceinline__ uint32_t group_or32(uint32_t x) {
-    if (G >= 2) x |= dpp32<0xB1>(x);   // quad_perm(1, 0, 3, 2): partner lane ^ 1
-    if (G >= 4) x |= dpp32<0x4E>(x);   // quad_perm(2, 3, 0, 1): partner lane ^ 2
+    if (G >= 2) x |= dpp32<0xB1>(x);    // quad_perm(1, 0, 3, 2): partner lane ^ 1
+    if (G >= 4) x |= dpp32<0x4E>(x);    // quad_perm(2, 3, 0, 1): partner lane ^ 2
+    if (G >= 8) x |= dpp32<0x141>(x);   // row_half_mirror: lane 7 - i of its 8 (quads 0 and 1)
+    if (G >= 16) x |= dpp32<0x140>(x);  // row_mirror: lane 15 - i of its 16 (halves 0 and 1)
     return x;
 }
 template <int G>
@@ -295,6 +297,8 @@ template <int G>
 __device__ __forceinline__ uint64_t group_min64(uint64_t x) {
     if (G >= 2) x = min64_dpp<0xB1>(x);
     if (G >= 4) x = min64_dpp<0x4E>(x);
+    if (G >= 8) x = min64_dpp<0x141>(x);
+    if (G >= 16) x = min64_dpp<0x140>(x);
     return x;
 }
 
@@ -327,7 +331,12 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const D
                     tm[1 + l] |= bits;
         }
     }
-    const uint64_t pat = (G == 4 ? 0x1111111111111111ull : G == 2 ? 0x5555555555555555ull : ~0ull) << u;
+    const uint64_t pat = (G == 16  ? 0x0001000100010001ull
+                          : G == 8 ? 0x0101010101010101ull
+                          : G == 4 ? 0x1111111111111111ull
+                          : G == 2 ? 0x5555555555555555ull
+                                   : ~0ull)
+                         << u;
     unsigned long long bk = ~0ull;
     for (uint64_t bits = group_or64<G>(tm[0]) & pat; bits; bits &= bits - 1ull) {
         const uint32_t k = (uint32_t)__builtin_ctzll(bits);
@@ -1019,12 +1028,16 @@ static void launch_merged_i(const KParams& P, const KParams* dP, const StepObjs&
 // slots per wave for a shard of `live` slots
 // (xrt_render_params.slots_per_wave overrides it; results do not depend on it)
 uint32_t step_merged_spw(const KParams& P, uint64_t live) {
+    const bool group = P.n_tris <= 64 && !(P.rflags & XRT_FLAG_NO_GROUP);   // 4 slots per wave: group traces only
+    if (P.spw_req == 4) return group ? 4u : 16u;
     if (P.spw_req == 16 || P.spw_req == 32 || P.spw_req == 64) return P.spw_req;
     // measured on C2 (tools/shard_sim.py): full waves down to ~160k live
-    // slots, 32 slots per wave down to ~90k, then 16 (4 lanes per slot)
+    // slots, 32 slots per wave down to ~90k, 16 (4 lanes per slot) down to kMergedLive16,
+    // then 4 (16 lanes per slot: the tail of a small shard, where a visit's latency, not
+    // issue, sets the time)
     if (live >= kMergedLive64) return 64;
     if (live >= kMergedLive32) return 32;
-    return 16;
+    return live >= kMergedLive16 || !group ? 16u : 4u;
 }
 
 // lanes that share one slot's traces at `spw` slots per wave (1 = pair passes over the wave)
@@ -1044,6 +1057,7 @@ static void launch_merged_spw(const KParams& P, const KParams* dP, const StepObj
     switch (step_merged_spw(P, live)) {
         case 64: if (lane64) XRT_MERGED_CASE(64, 1, true); else XRT_MERGED_CASE(64, 1, false); break;
         case 32: if (group) XRT_MERGED_CASE(32, 2, true); else XRT_MERGED_CASE(32, 1, false); break;
+        case 4: XRT_MERGED_CASE(4, 16, true); break;   // only with group traces (step_merged_spw)
         default: if (group) XRT_MERGED_CASE(16, 4, true); else XRT_MERGED_CASE(16, 1, false); break;
     }
 #undef XRT_MERGED_CASE

@@ -36,6 +36,10 @@ constexpr uint32_t kMergedVisits = 64; // merged-trace schedule: segments per sl
                                        // clamped so a launch's draws fit one refill block)
 constexpr uint32_t kMergedLive64 = 160000;  // merged-trace schedule: live slots for 64 slots per wave
 constexpr uint32_t kMergedLive32 = 90000;   // ... and for 32 (below: 16 slots, 4 lanes each)
+#ifndef XRT_LIVE16
+#define XRT_LIVE16 20000
+#endif
+constexpr uint32_t kMergedLive16 = XRT_LIVE16;   // ... and for 16 (below: 4 slots, 16 lanes each)
 constexpr uint32_t kStepRefill = 1;  // fused schedule: k_refill after every k_step
 constexpr uint32_t kVisitDraws = 13; // max RNG draws of one GI/Direct segment (4 lights)
 // fused schedule: a slot queues a refill when fewer than refill * visits * 13 + kRngVisit

@@ -808,55 +808,63 @@ __device__ __forceinline__ bool isnan3(v3 a) {
 }
 
 // HeterogeneousMedium::sampleMedium — delta tracking with spectral MIS (Src/medium.cpp:
-// 45-133), resumable: returns 0 = left the medium, 1 = real scattering, 2 = suspended
-// because fewer than 8 RNG words remain (the slot resumes after the next refill).
-// `t`, `tt` (throughput_tracking) and `sa` (sigma_a) carry the loop state.
-__device__ int delta_track(const KParams& P, v3 o, v3 d, v3 thr, float& t, float t1, v3& tt, v3& sa, Rng& rng,
-                           uint32_t g, v3& pos, v3& dir, v3& tm) {
+// 45-133), one collision per call: returns 0 = left the medium, 1 = real scattering,
+// 2 = suspended because fewer than 8 RNG words remain (the slot resumes after the next
+// refill), 3 = null collision (call again).  `t`, `tt` (throughput_tracking) and `sa`
+// (sigma_a) carry the loop state.
+__device__ __forceinline__ int delta_step(const KParams& P, v3 o, v3 d, v3 thr, float& t, float t1, v3& tt, v3& sa,
+                                          Rng& rng, uint32_t g, v3& pos, v3& dir, v3& tm) {
     const DMedium& M = P.medium;
     const float majorant = M.majorant, invMajorant = M.inv_majorant;
     const v3 vmaj = mk(majorant, majorant, majorant);
     const v3 absorb = ld3(M.absorption), scatter = ld3(M.scattering);
-    for (;;) {
-        if (g - rng.c < 8u) return 2;
-        v3 pmf;
-        const uint32_t channel = sample_wavelength(thr * tt, (vmaj - sa) * invMajorant, rng, pmf);
-        const float s = -glibc_logf(smax(1.0f - rng.next(), 0.0f)) * invMajorant;
-        t += s;
-        if (t > t1 - kRAY_EPS) {
-            pos = ray_at(o, d, t1 + kRAY_EPS);
-            dir = d;
-            const float dist = s - (t - (t1 - kRAY_EPS));
-            const float e = glibc_expf(-majorant * dist);   // vexp((-vmaj) * dist)
-            const v3 tr = mk(e, e, e);
-            const v3 pdf = pmf * tr;
-            tt = tt * (tr / (pdf.x + pdf.y + pdf.z));
-            tm = isnan3(tt) ? mk(0, 0, 0) : tt;
-            return 0;
-        }
-        const float density = medium_density(M, ray_at(o, d, t));
-        const v3 sigma_s = scatter * density;
-        sa = absorb * density;
-        const v3 sigma_n = (vmaj - sa) - sigma_s;
-        const v3 den = sigma_s + sigma_n;
-        // P_s = sigma_s / (sigma_s + sigma_n): the acceptance test reads one component, the
-        // scattering branch all three (the same quotients, computed where they are used)
-        if (rng.next() < comp(sigma_s, channel) / comp(den, channel)) {
-            const v3 P_s = sigma_s / den;
-            pos = ray_at(o, d, t);
-            hg_sample(M.g, d, rng, dir);
-            const float e = glibc_expf(-majorant * s);   // vexp((-vmaj) * s): three equal arguments
-            const v3 tr = mk(e, e, e);
-            const v3 pdf = (pmf * (tr * majorant)) * P_s;
-            tt = tt * ((tr * sigma_s) / (pdf.x + pdf.y + pdf.z));
-            tm = isnan3(tt) ? mk(0, 0, 0) : tt;
-            return 1;
-        }
-        const v3 P_n = sigma_n / den;
-        const float e = glibc_expf(-majorant * s);
+    if (g - rng.c < 8u) return 2;
+    v3 pmf;
+    const uint32_t channel = sample_wavelength(thr * tt, (vmaj - sa) * invMajorant, rng, pmf);
+    const float s = -glibc_logf(smax(1.0f - rng.next(), 0.0f)) * invMajorant;
+    t += s;
+    if (t > t1 - kRAY_EPS) {
+        pos = ray_at(o, d, t1 + kRAY_EPS);
+        dir = d;
+        const float dist = s - (t - (t1 - kRAY_EPS));
+        const float e = glibc_expf(-majorant * dist);   // vexp((-vmaj) * dist)
         const v3 tr = mk(e, e, e);
-        const v3 pdf = (pmf * (tr * majorant)) * P_n;
-        tt = tt * ((tr * sigma_n) / (pdf.x + pdf.y + pdf.z));
+        const v3 pdf = pmf * tr;
+        tt = tt * (tr / (pdf.x + pdf.y + pdf.z));
+        tm = isnan3(tt) ? mk(0, 0, 0) : tt;
+        return 0;
+    }
+    const float density = medium_density(M, ray_at(o, d, t));
+    const v3 sigma_s = scatter * density;
+    sa = absorb * density;
+    const v3 sigma_n = (vmaj - sa) - sigma_s;
+    const v3 den = sigma_s + sigma_n;
+    // P_s = sigma_s / (sigma_s + sigma_n): the acceptance test reads one component, the
+    // scattering branch all three (the same quotients, computed where they are used)
+    if (rng.next() < comp(sigma_s, channel) / comp(den, channel)) {
+        const v3 P_s = sigma_s / den;
+        pos = ray_at(o, d, t);
+        hg_sample(M.g, d, rng, dir);
+        const float e = glibc_expf(-majorant * s);   // vexp((-vmaj) * s): three equal arguments
+        const v3 tr = mk(e, e, e);
+        const v3 pdf = (pmf * (tr * majorant)) * P_s;
+        tt = tt * ((tr * sigma_s) / (pdf.x + pdf.y + pdf.z));
+        tm = isnan3(tt) ? mk(0, 0, 0) : tt;
+        return 1;
+    }
+    const v3 P_n = sigma_n / den;
+    const float e = glibc_expf(-majorant * s);
+    const v3 tr = mk(e, e, e);
+    const v3 pdf = (pmf * (tr * majorant)) * P_n;
+    tt = tt * ((tr * sigma_n) / (pdf.x + pdf.y + pdf.z));
+    return 3;
+}
+// the whole walk (0, 1 or 2 as delta_step)
+__device__ int delta_track(const KParams& P, v3 o, v3 d, v3 thr, float& t, float t1, v3& tt, v3& sa, Rng& rng,
+                           uint32_t g, v3& pos, v3& dir, v3& tm) {
+    for (;;) {
+        const int r = delta_step(P, o, d, thr, t, t1, tt, sa, rng, g, pos, dir, tm);
+        if (r != 3) return r;
     }
 }
 
