@@ -410,7 +410,13 @@ __global__ __launch_bounds__(kBlock) void k_trace_2a_coop(KParams P, const StepO
         }
         unsigned long long best;
         uint32_t occ;
+#ifdef XRT_PHASE_CLOCK
+        uint64_t ph_acc[16] = {};
+        uint32_t ph_cnt[3] = {};
+        merged_trace<NL>(SO, L, W, lane, want, o, d, smask, so, sd, stm, best, occ, ph_acc, ph_cnt);
+#else
         merged_trace<NL>(SO, L, W, lane, want, o, d, smask, so, sd, stm, best, occ);
+#endif
         float bt = kINF, bu = 0.0f, bv = 0.0f;
         int bk = -1;
         if (want && best != ~0ull) {

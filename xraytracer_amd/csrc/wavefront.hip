@@ -757,14 +757,36 @@ __device__ float medium_density(const DMedium& M, v3 p) {
     return vdb_interp(M, C, q);
 }
 
+// Component-wise quotients a / b and a / (b, b, b) with one division when the numerators (and
+// denominators) are the same bits — achromatic media and throughputs (C5) — else three; the
+// same IEEE quotients either way.  Bit equality, not ==: +0 and -0 differ in the quotient.
+__device__ __forceinline__ bool same3(v3 a) {
+    return __float_as_uint(a.x) == __float_as_uint(a.y) && __float_as_uint(a.y) == __float_as_uint(a.z);
+}
+__device__ __forceinline__ v3 div3s(v3 a, float b) {
+    if (same3(a)) {
+        const float q = a.x / b;
+        return mk(q, q, q);
+    }
+    return a / b;
+}
+__device__ __forceinline__ v3 div3v(v3 a, v3 b) {
+    if (same3(a) && same3(b)) {
+        const float q = a.x / b.x;
+        return mk(q, q, q);
+    }
+    return a / b;
+}
+
 // Medium::sampleWavelength + DiscreteEmpiricalDistribution1D (Src/medium.h:102-115,
 // Src/sampler.h:53-94).  lower_bound past the end is UB in the reference; clamped to 2.
 __device__ __forceinline__ uint32_t sample_wavelength(v3 thr, v3 albedo, Rng& rng, v3& pmf) {
     const v3 ta = thr * albedo;
     const float sum = ((0.0f + ta.x) + ta.y) + ta.z;
-    const float c1 = 0.0f + ta.x / sum;
-    const float c2 = c1 + ta.y / sum;
-    const float c3 = c2 + ta.z / sum;
+    const v3 q = div3s(ta, sum);   // ta.x / sum, ta.y / sum, ta.z / sum
+    const float c1 = 0.0f + q.x;
+    const float c2 = c1 + q.y;
+    const float c3 = c2 + q.z;
     pmf = mk(c1 - 0.0f, c2 - c1, c3 - c2);
     const float u = rng.next();
     int x = 0;
@@ -830,7 +852,7 @@ __device__ __forceinline__ int delta_step(const KParams& P, v3 o, v3 d, v3 thr, 
         const float e = glibc_expf(-majorant * dist);   // vexp((-vmaj) * dist)
         const v3 tr = mk(e, e, e);
         const v3 pdf = pmf * tr;
-        tt = tt * (tr / (pdf.x + pdf.y + pdf.z));
+        tt = tt * div3s(tr, pdf.x + pdf.y + pdf.z);
         tm = isnan3(tt) ? mk(0, 0, 0) : tt;
         return 0;
     }
@@ -842,21 +864,21 @@ __device__ __forceinline__ int delta_step(const KParams& P, v3 o, v3 d, v3 thr, 
     // P_s = sigma_s / (sigma_s + sigma_n): the acceptance test reads one component, the
     // scattering branch all three (the same quotients, computed where they are used)
     if (rng.next() < comp(sigma_s, channel) / comp(den, channel)) {
-        const v3 P_s = sigma_s / den;
+        const v3 P_s = div3v(sigma_s, den);
         pos = ray_at(o, d, t);
         hg_sample(M.g, d, rng, dir);
         const float e = glibc_expf(-majorant * s);   // vexp((-vmaj) * s): three equal arguments
         const v3 tr = mk(e, e, e);
         const v3 pdf = (pmf * (tr * majorant)) * P_s;
-        tt = tt * ((tr * sigma_s) / (pdf.x + pdf.y + pdf.z));
+        tt = tt * div3s(tr * sigma_s, pdf.x + pdf.y + pdf.z);
         tm = isnan3(tt) ? mk(0, 0, 0) : tt;
         return 1;
     }
-    const v3 P_n = sigma_n / den;
+    const v3 P_n = div3v(sigma_n, den);
     const float e = glibc_expf(-majorant * s);
     const v3 tr = mk(e, e, e);
     const v3 pdf = (pmf * (tr * majorant)) * P_n;
-    tt = tt * ((tr * sigma_n) / (pdf.x + pdf.y + pdf.z));
+    tt = tt * div3s(tr * sigma_n, pdf.x + pdf.y + pdf.z);
     return 3;
 }
 // the whole walk (0, 1 or 2 as delta_step)
@@ -913,21 +935,21 @@ __device__ int homog_track(const KParams& P, v3 o, v3 d, v3 thr, float t0, float
     if (M.kind == XRT_MEDIUM_HOMOGENEOUS_MIS) {
         // HomogeneousMediumMIS::sampleMedium (Src/medium.h:154-191)
         v3 pmf;
-        const uint32_t channel = sample_wavelength(thr, ss / st, rng, pmf);
+        const uint32_t channel = sample_wavelength(thr, div3v(ss, st), rng, pmf);
         const float t = -glibc_logf(smax(1.0f - rng.next(), 0.0f)) / comp(st, channel);
         if (t > distToSurface - kRAY_EPS) {
             pos = ray_at(o, d, t1 + kRAY_EPS);
             dir = d;
             const v3 tr = analytic_tr(distToSurface, st);
             const v3 pdf = pmf * tr;
-            tm = tr / (pdf.x + pdf.y + pdf.z);
+            tm = div3s(tr, pdf.x + pdf.y + pdf.z);
             return 0;
         }
         hg_sample(M.g, d, rng, dir);
         pos = ray_at(o, d, t0 + t);
         const v3 tr = analytic_tr(t, st);
         const v3 pdf = pmf * (st * tr);
-        tm = (tr * ss) / (pdf.x + pdf.y + pdf.z);
+        tm = div3s(tr * ss, pdf.x + pdf.y + pdf.z);
         return 1;
     }
     if (M.kind == XRT_MEDIUM_HOMOGENEOUS_ACHROMATIC) {
@@ -941,7 +963,7 @@ __device__ int homog_track(const KParams& P, v3 o, v3 d, v3 thr, float t0, float
         }
         hg_sample(M.g, d, rng, dir);
         pos = ray_at(o, d, t0 + t);
-        tm = ss / st;
+        tm = div3v(ss, st);
         return 1;
     }
     // HomogeneousMediumNoMIS::sampleMedium (Src/medium.h:240-275)
@@ -1750,7 +1772,7 @@ __global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, con
                         if (depth > 0) {
                             const float pr = smin((thr.x + thr.y + thr.z) / 3.0f, 1.0f);
                             if (rng.next() >= pr) alive = false, ended = true;
-                            else thr = thr / mk(pr, pr, pr);
+                            else thr = div3s(thr, pr);   // thr / Vec3f(pr): one division when achromatic
                         }
                         const DObj& ob = L.obj[obj];
                         if (alive && ob.light >= 0) {
