@@ -35,7 +35,10 @@ constexpr uint32_t kStepVisits = 32; // fused schedule: path segments per slot p
 constexpr uint32_t kMergedVisits = 64; // merged-trace schedule: segments per slot per launch (at most;
                                        // clamped so a launch's draws fit one refill block)
 constexpr uint32_t kMergedLive64 = 160000;  // merged-trace schedule: live slots for 64 slots per wave
-constexpr uint32_t kMergedLive32 = 90000;   // ... and for 32 (below: 16 slots, 4 lanes each)
+#ifndef XRT_LIVE32
+#define XRT_LIVE32 90000
+#endif
+constexpr uint32_t kMergedLive32 = XRT_LIVE32;   // ... and for 32 (below: 16 slots, 4 lanes each)
 #ifndef XRT_LIVE16
 #define XRT_LIVE16 20000
 #endif

@@ -1757,7 +1757,7 @@ __global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, con
                             const bool vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias CNT_ARG);
                             const float cosv = smax(0.0f, dot(S.ng, wi));
                             const v3 fr = eval_bxdf(ob);
-                            rad = rad + (((fr * (float)vis) * Lv) * cosv) / pdf;
+                            rad = rad + div3s(((fr * (float)vis) * Lv) * cosv, pdf);
                         }
                     }
                     ended = true;

@@ -446,6 +446,18 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
             big.resize(P.n_tris);
             for (size_t t = 0; t < big.size(); ++t) big[t] = (uint32_t)t;
         }
+        // A triangle with an exactly zero edge vector (two equal vertices, e.g. half of a
+        // SphereMesh's pole cells) is rejected by every Moller-Trumbore test: e1 = 0 makes
+        // det = e1 . pvec an exact 0, e2 = 0 makes pvec = d x e2 an exact 0 (a NaN direction
+        // fails t > eps instead) — so it is left out of the BVH, where its box would overlap
+        // every other pole triangle's.
+        {
+            auto zero = [](const f4& e) { return e.x == 0.0f && e.y == 0.0f && e.z == 0.0f; };
+            size_t w = 0;
+            for (size_t i = 0; i < big.size(); ++i)
+                if (!zero(tri[3 * big[i] + 1]) && !zero(tri[3 * big[i] + 2])) big[w++] = big[i];
+            if (w > 0) big.resize(w);
+        }
         const size_t nt = big.size();
         std::vector<float> mn(3 * nt), mx(3 * nt);
         float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
