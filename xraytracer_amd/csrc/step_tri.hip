@@ -370,8 +370,11 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const D
 // the (t bits << 32 | local index) minimum is the (t, original index) minimum).  The winner's
 // (t, u, v) are recomputed with Mesh::rayTriangleIntersect's ops as the merged kernel does;
 // rays whose segment reaches the BVH root are queued for k_trace_deep.
+#ifndef XRT_2A_WAVES
+#define XRT_2A_WAVES 1
+#endif
 template <int NL>
-__global__ __launch_bounds__(kBlock) void k_trace_2a_coop(KParams P, const StepObjs SO, const uint32_t* __restrict__ list,
+__global__ __launch_bounds__(kBlock, XRT_2A_WAVES) void k_trace_2a_coop(KParams P, const StepObjs SO, const uint32_t* __restrict__ list,
                                                           const uint32_t* __restrict__ count, uint32_t* zero_count) {
     extern __shared__ __attribute__((aligned(16))) f4 lds_2c[];
     LScene L;

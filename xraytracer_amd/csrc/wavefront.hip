@@ -18,6 +18,15 @@
 #include "bvh.h"
 #include "path_common.h"
 
+// minimum waves per SIMD the wavefront kernels are compiled for (launch bounds; experiment
+// builds override them)
+#ifndef XRT_SHADE_WAVES
+#define XRT_SHADE_WAVES 1
+#endif
+#ifndef XRT_DEEP_WAVES
+#define XRT_DEEP_WAVES 1
+#endif
+
 namespace xrt {
 
 
@@ -477,7 +486,7 @@ __device__ __forceinline__ bool bvh_leaf_batch(const KParams& P, int first, int 
 // stacked.  Exact for the same reason as bvh_trace: every triangle whose padded box overlaps
 // [0, best t] is tested, whatever the order.
 template <typename SE>
-__global__ __launch_bounds__(kBlock) void k_trace_deep4(KParams P) {
+__global__ __launch_bounds__(kBlock, XRT_DEEP_WAVES) void k_trace_deep4(KParams P) {
     extern __shared__ uint32_t bvh_stack_lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int ntop = P.bvh4_nodes < (int)kBvhTopNodes ? P.bvh4_nodes : (int)kBvhTopNodes;
@@ -989,7 +998,7 @@ __device__ int homog_track(const KParams& P, v3 o, v3 d, v3 thr, float t0, float
 
 // =================================================================== k_shade ====
 template <int SCN, int INTEG>
-__global__ __launch_bounds__(kBlock) void k_shade(KParams P, const uint32_t* __restrict__ list,
+__global__ __launch_bounds__(kBlock, XRT_SHADE_WAVES) void k_shade(KParams P, const uint32_t* __restrict__ list,
                                                    const uint32_t* __restrict__ count, uint32_t* __restrict__ out,
                                                    uint32_t* out_count, uint32_t* req_count) {
     const PartIter it = part_iter(P, count, kBlock);
