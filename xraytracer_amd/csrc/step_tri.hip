@@ -466,108 +466,6 @@ hipError_t launch_trace_2a_coop(const KParams& P, const uint32_t* list, const ui
 // current one twists, and the slot state is not touched — the merged kernel clears
 // ST_RNGREQ when it next loads the slot, which is always after this kernel (one refill
 // launch follows every step launch).
-// One twist of a slot's ring by a whole wave, staged through LDS: the old block (624 words,
-// 16-byte aligned because kRing*4 and kMT*4 are multiples of 16) comes in as 156 dwordx4
-// loads (3 instructions per wave) and every recurrence operand is then an LDS read, instead
-// of 26 overlapping global_load_dword per lane whose 64-lane requests re-fetch each cache
-// line ~2.6 times through the TA.  The new words go out as 11 coalesced dword stores.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-struct Staged { u32x4 v[3]; };
-
-__device__ __forceinline__ Staged load_block(const uint32_t* ring, uint32_t g, int lane) {
-    const u32x4* old = reinterpret_cast<const u32x4*>(ring + (kMT - g % kRing));
-    Staged r;
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-        r.v[k] = __builtin_nontemporal_load(old + min((uint32_t)lane + 64u * k, (uint32_t)(kMT / 4 - 1)));
-    return r;
-}
-
-__device__ __forceinline__ void store_block(const Staged& r, int lane, uint32_t* lds) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const uint32_t q = (uint32_t)lane + 64u * k;
-        if (q < kMT / 4) reinterpret_cast<u32x4*>(lds)[q] = r.v[k];
-    }
-    wave_sync();
-}
-
-// The new block goes back out through the same LDS buffer (its old words are all in
-// registers by then) as 156 dwordx4 stores: whole 64-byte runs instead of 11 dword stores
-// per lane that start at arbitrary offsets within a cache line.
-__device__ __forceinline__ void twist_block(uint32_t* ring, uint32_t g, int lane, uint32_t* buf) {
-    const uint32_t* old = buf;
-    uint32_t x0[4], x1[4], x397[4], y0[4], y1[4], z0[3], z1[3];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t m = min((uint32_t)lane + 64u * j, 226u);
-        x0[j] = old[m], x1[j] = old[m + 1], x397[j] = old[m + 397];
-        y0[j] = old[227 + m], y1[j] = old[228 + m];
-    }
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const uint32_t m = min((uint32_t)lane + 64u * j, 169u);
-        z0[j] = old[454 + m], z1[j] = old[min(455 + m, kMT - 1)];
-    }
-    uint32_t a[4], b[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) a[j] = x397[j] ^ mt_mix(x0[j], x1[j]);
-    const uint32_t n0 = __builtin_amdgcn_readfirstlane(a[0]);   // x[g]: the new block's first word
-#pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = a[j] ^ mt_mix(y0[j], y1[j]);
-    wave_sync();   // every old word is in registers before the buffer is overwritten
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const uint32_t m = (uint32_t)lane + 64u * j;
-        if (m < 170u) buf[454 + m] = b[j] ^ mt_mix(z0[j], m + 455 < kMT ? z1[j] : n0);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t m = (uint32_t)lane + 64u * j;
-        if (m < 227u) buf[m] = a[j], buf[227 + m] = b[j];
-    }
-    wave_sync();
-    u32x4* nw = reinterpret_cast<u32x4*>(ring + g % kRing);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const uint32_t q = (uint32_t)lane + 64u * k;
-        if (q < kMT / 4) nw[q] = reinterpret_cast<const u32x4*>(buf)[q];
-    }
-}
-
-// Inline refill (the merged schedule): at the end of a step launch each wave twists the
-// rings of its own slots that are running low, one slot at a time through `buf` (the
-// wave's trace scratch, idle by then), the next slot's old block loading into registers
-// while the current one twists — instead of queueing them for a separate k_refill_merged
-// launch after every step launch (6 ms of an 80 ms C2 frame, serialised).  Safe for the
-// unconsumed words: a slot asks when fewer than rng_keep (<= 624) words are left, so the
-// new block x[g, g + 624) overwrites only words the slot has already drawn.
-__device__ __forceinline__ void wave_refill(const KParams& P, bool want, uint32_t s, uint32_t g, int lane,
-                                            uint32_t* buf) {
-    uint64_t rq = __ballot(want);
-    if (!rq) return;
-    int l = __builtin_ctzll(rq);
-    rq &= rq - 1ull;
-    uint32_t sc = (uint32_t)__builtin_amdgcn_readlane((int)s, l), gc = (uint32_t)__builtin_amdgcn_readlane((int)g, l);
-    Staged blk = load_block(P.ring + (size_t)sc * kRing, gc, lane);
-    for (;;) {
-        store_block(blk, lane, buf);
-        const bool more = rq != 0ull;
-        uint32_t sn = sc, gn = gc;
-        if (more) {
-            l = __builtin_ctzll(rq);
-            rq &= rq - 1ull;
-            sn = (uint32_t)__builtin_amdgcn_readlane((int)s, l), gn = (uint32_t)__builtin_amdgcn_readlane((int)g, l);
-            blk = load_block(P.ring + (size_t)sn * kRing, gn, lane);
-        }
-        twist_block(P.ring + (size_t)sc * kRing, gc, lane, buf);
-        if (lane == 0) P.rng_g[sc] = gc + kMT;
-        if (!more) break;
-        wave_sync();
-        sc = sn, gc = gn;
-    }
-}
-
 #ifdef XRT_PHASE_CLOCK
 #define PH_TARGS , ph_acc, ph_cnt
 #define MPH_DECL uint64_t ph_t = __builtin_amdgcn_s_memtime();

@@ -8,9 +8,10 @@
 //   slots  : one path slot per pixel of this shard; all per-slot state is SoA (float4 /
 //            uint32 arrays indexed by slot) so a wave's loads are coalesced.
 //   RNG    : per slot a 1248-word ring (two 624-word mt19937 blocks) + cursor/generated
-//            counters.  A shading visit that finds fewer than kRngMin words left puts the
-//            slot on a refill list; k_refill (every kRefillEvery launches) twists each
-//            listed ring with one whole wave, all listed slots in parallel.
+//            counters.  A k_shade visit that finds fewer than kRngMin words left has its
+//            wave twist the slot's next block at the end of the same launch (wave_refill);
+//            the fused schedules put the slot on a refill list that k_refill_merged twists,
+//            one whole wave per listed ring.
 #pragma once
 #include <stdint.h>
 
@@ -30,7 +31,6 @@ constexpr uint32_t kRngVisit = 16;   // a slot visit needs at least this many (m
                                      // GI/Direct visit with kMaxLights lights is 13; VPT walks
                                      // suspend themselves below 8)
 constexpr uint32_t kMaxParts = 64;   // live-list partitions (counters per list)
-constexpr uint32_t kRefillEvery = 4; // wavefront schedule: k_refill after every 4th k_shade
 constexpr uint32_t kStepVisits = 32; // fused schedule: path segments per slot per k_step
 constexpr uint32_t kMergedVisits = 64; // merged-trace schedule: segments per slot per launch (at most;
                                        // clamped so a launch's draws fit one refill block)

@@ -1001,6 +1001,7 @@ template <int SCN, int INTEG>
 __global__ __launch_bounds__(kBlock, XRT_SHADE_WAVES) void k_shade(KParams P, const uint32_t* __restrict__ list,
                                                    const uint32_t* __restrict__ count, uint32_t* __restrict__ out,
                                                    uint32_t* out_count, uint32_t* req_count) {
+    __shared__ __attribute__((aligned(16))) uint32_t rbuf[kBlock / 64][kMT];   // wave_refill staging
     const PartIter it = part_iter(P, count, kBlock);
     const int tid = threadIdx.x, lane = tid & 63;
     for (uint32_t base = it.first; base < it.n; base += it.stride) {
@@ -1010,12 +1011,12 @@ __global__ __launch_bounds__(kBlock, XRT_SHADE_WAVES) void k_shade(KParams P, co
         const uint32_t g = valid ? P.rng_g[s] : 0;
         Rng rng{P.ring + (size_t)s * kRing, valid ? P.rng_c[s] : 0};
         uint32_t st = valid ? P.state[s] : ST_DONE;
-        // RNG words: request a refill below kRngMin, sit this launch out below kRngVisit
+        // RNG words: below kRngMin the wave twists the slot's next block at the end of this
+        // launch (wave_refill below; the block overwrites ring words < g - 624 <= c, all
+        // drawn); below kRngVisit the slot sits this launch out
         const uint32_t avail = g - rng.c;
-        const bool want_req = valid && avail < kRngMin && !(st & ST_RNGREQ);
-        if (want_req) st |= ST_RNGREQ;
+        const bool want_req = valid && avail < kRngMin;
         const bool go = valid && avail >= kRngVisit;
-        if (valid && !go && want_req) P.state[s] = st;
         if (go) {
             rng.prefetch(avail);
             uint32_t depth = P.depth[s];
@@ -1326,10 +1327,12 @@ __global__ __launch_bounds__(kBlock, XRT_SHADE_WAVES) void k_shade(KParams P, co
             if (nrej) P.c_rej[s] += nrej;
             if (nstall) P.c_stall[s] += nstall;
         }
-        // ---- 4. compaction + refill requests: ballot + prefix count, one atomic per wave
+        // ---- 4. compaction (ballot + prefix count, one atomic per wave), then the wave's
+        // refills in-line, overlapping other waves' shading instead of a serial k_refill
         wave_append(valid && !(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
-        wave_append(want_req, s, P.req + it.p * P.part_cap, req_count + it.p, lane);
+        wave_refill(P, want_req && !(st & ST_DONE), s, g, lane, rbuf[tid >> 6]);
     }
+    (void)req_count;
 }
 
 // Debug instrumentation (-DXRT_COUNT_TESTS, experiment builds only): triangle tests done

@@ -830,8 +830,8 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     // Schedule: the fused k_step (scene resident in LDS, kStepVisits path segments per
     // slot per launch, in-kernel compaction and refill requests; k_refill every
     // kStepRefill rounds) when the scene fits, else the multi-pass wavefront (k_shade, then
-    // k_trace streaming the scene through LDS tiles, k_refill every kRefillEvery
-    // iterations).  k_step rotates three live counters: round i reads counts[i%3], appends
+    // k_trace streaming the scene through LDS tiles; k_shade refills its slots' rings
+    // in-line).  k_step rotates three live counters: round i reads counts[i%3], appends
     // to counts[(i+1)%3] and clears counts[(i+2)%3] for round i+1.
     const bool fused = !(p->flags & XRT_FLAG_WAVEFRONT) && step_lds_bytes(P) != 0;
     const bool merged = fused && !(p->flags & XRT_FLAG_NO_MERGED) && use_step_merged(P);
@@ -893,10 +893,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
                 return launch_trace(P, lists[nxt], counts_at(nxt), counts_at(cur), blocks, c->stream);
             });
             if (e != hipSuccess) return hip_err(c, e, "k_trace");
-            if (it % kRefillEvery == kRefillEvery - 1) {
-                e = refill();
-                if (e != hipSuccess) return hip_err(c, e, "k_refill");
-            }
+            // no k_refill: k_shade twists its slots' rings itself (wave_refill)
         }
         if (it % poll_every == poll_every - 1) {
             const int ps = poll_slot++ % 8;
