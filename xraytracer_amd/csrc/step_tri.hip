@@ -18,7 +18,8 @@
 //    they resolve (rad_fin), while its successor's camera ray is traced.
 //  * Object-major pair passes: for each object (kernel-argument record, scalar loads) the
 //    wave ballots which of its rays (1 + NL per lane) overlap the object's culling box,
-//    ranks them (mbcnt, one LDS word each) and tests the (ray, triangle) pairs 64 per pass,
+//    ranks those rays into LDS (mbcnt; origin + tmax, direction + ray id) and tests the
+//    (ray, triangle) pairs 64 per pass,
 //    pair j -> ray rank j / count (magic multiply), triangle first + j % count.  No prefix
 //    scan, no per-lane expansion loop.  Closest hits merge with an LDS atomicMin of
 //    (t bits << 32 | triangle): smallest t, ties to the lower triangle index — the
@@ -122,11 +123,10 @@ __host__ __device__ inline uint32_t merged_wave_off(const KParams& P, const Step
 template <int NL>
 struct MergedWave {
     static constexpr int R = 1 + NL;   // rays per lane: extension + one shadow ray per light
-    f4 ro[R * 64];                     // origin, w = tmax (shadow rays)
-    f4 rd[R * 64];
+    f4 ro[R * 64];                     // the current object's rays, ranked: origin, w = tmax
+    f4 rd[R * 64];                     // direction, w = ray id q * 64 + lane (bits)
     unsigned long long best[64];       // closest hit of the extension ray: (t bits << 32) | tri
     uint32_t occ[64];                  // bit l: shadow ray l is occluded
-    uint32_t list[R * 64];             // ranked rays (q * 64 + lane) of the current object
 };
 
 // A float that is +0, -0 or NaN as a 2-bit code (0, 1, 2) and back (NaN: the canonical
@@ -196,7 +196,7 @@ __device__ __forceinline__ bool ray_tri_nb(v3 o, v3 d, v3 v0, v3 e1, v3 e2, floa
 }
 
 // One cooperative trace of the wave: the extension ray (closest hit, if `ext`) and the
-// pending shadow rays (any hit, bits of `shm`; already stored in W by the shading code).
+// pending shadow rays (any hit, bits of `shm`).
 template <int NL>
 __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L, MergedWave<NL>& W, int lane,
                                              bool ext, v3 o, v3 d, uint32_t shm, const v3 (&so)[NL + 1],
@@ -209,8 +209,6 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
     constexpr int R = 1 + NL;
     W.best[lane] = ~0ull;
     W.occ[lane] = 0u;
-    W.ro[lane] = make_float4(o.x, o.y, o.z, kINF);
-    W.rd[lane] = make_float4(d.x, d.y, d.z, 0.0f);
     v3 inv[R], oi[R];
     inv[0] = rcp3c(d);
     oi[0] = o * inv[0];
@@ -226,11 +224,18 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
         for (int l = 0; l < NL; ++l)
             need[1 + l] = B.occluder && ((shm >> l) & 1u) && !plane_away(so[l], sd[l], B.axis, B.plane) &&
                           obj_overlap(oi[1 + l], inv[1 + l], B, stm[l]);
+        // the rays themselves are ranked into W (not their ids), so a pair reads its ray
+        // with one LDS access instead of an id and then the ray
         uint32_t tot = 0;
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const uint64_t m = __ballot(need[q]);
-            if (need[q]) W.list[tot + lanemask_rank(m)] = (uint32_t)(q * 64 + lane);
+            if (need[q]) {
+                const uint32_t at = tot + lanemask_rank(m);
+                const v3 ro = q == 0 ? o : so[q - 1], rd = q == 0 ? d : sd[q - 1];
+                W.ro[at] = make_float4(ro.x, ro.y, ro.z, q == 0 ? kINF : stm[q - 1]);
+                W.rd[at] = make_float4(rd.x, rd.y, rd.z, __uint_as_float((uint32_t)(q * 64 + lane)));
+            }
             tot += (uint32_t)__popcll(m);
         }
         if (tot == 0) continue;
@@ -245,9 +250,9 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
             if (j < pairs) {
                 const uint32_t r = (c == 1u) ? j : __umulhi(j, magic);
                 const uint32_t k = first + (j - r * c);
-                const uint32_t e = W.list[r];
-                const f4 A = W.ro[e];
-                const f4 D = W.rd[e];
+                const f4 A = W.ro[r];
+                const f4 D = W.rd[r];
+                const uint32_t e = __float_as_uint(D.w);
                 float t;
                 const bool hit = ray_tri_nb(xyz(A), xyz(D), xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]),
                                             xyz(L.tri[3 * k + 2]), t);
@@ -408,8 +413,6 @@ __global__ __launch_bounds__(kBlock, XRT_2A_WAVES) void k_trace_2a_coop(KParams 
                 so[l] = xyz(a), stm[l] = a.w;
                 sd[l] = xyz(P.sh_d[(size_t)l * P.n_slots + s]);
             }
-            W.ro[(1 + l) * 64 + lane] = make_float4(so[l].x, so[l].y, so[l].z, stm[l]);
-            W.rd[(1 + l) * 64 + lane] = make_float4(sd[l].x, sd[l].y, sd[l].z, 0.0f);
         }
         unsigned long long best;
         uint32_t occ;
@@ -714,10 +717,6 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                             shm |= 1u << l;
                             const float bias = 0.01f;
                             so[l] = pos + ng * bias, sd[l] = wi, stm[l] = tmax - bias;
-                            if constexpr (!LANE) {
-                                W.ro[(1 + l) * 64 + lane] = make_float4(so[l].x, so[l].y, so[l].z, stm[l]);
-                                W.rd[(1 + l) * 64 + lane] = make_float4(wi.x, wi.y, wi.z, 0.0f);
-                            }
                             const float cosv = smax(0.0f, dot(ng, wi));
                             // vis * fr * L * cos / pdf (Src/integrator.h:250-262) for vis = 1, 0.
                             // fr * 1 == fr; for vis = 0 the product is +-0 or NaN and pdf is

@@ -839,7 +839,11 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     // sets visits_per_launch (results do not depend on it)
     const uint32_t merged_visits =
         merged ? std::min<uint32_t>(kMergedVisits, (kMT - step_merged_draws(P)) / step_merged_draws(P)) : 0;
-    const uint32_t step_visits = p->visits_per_launch ? p->visits_per_launch : merged ? merged_visits : kStepVisits;
+    const char* ev = exp_env("XRT_VISITS");   // experiment builds only
+    const uint32_t step_visits = ev                    ? (uint32_t)std::atoi(ev)
+                                 : p->visits_per_launch ? p->visits_per_launch
+                                 : merged               ? merged_visits
+                                                        : kStepVisits;
     // the merged kernel relies on one refill launch after every step launch (it clears
     // ST_RNGREQ itself)
     const uint32_t step_refill = merged ? 1u : kStepRefill;
