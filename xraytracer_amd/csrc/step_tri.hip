@@ -181,11 +181,15 @@ __device__ __forceinline__ bool plane_away(v3 o, v3 d, int axis, float c) {
 }
 
 // Mesh::rayTriangleIntersect (Src/primitive.cpp:140-168) without branches: the same float
-// operations, and the same accept/reject decisions (NaN comparisons included).
+// operations, and the same accept/reject decisions (NaN comparisons included).  invDet is
+// the Newton reciprocal without the IEEE fallback: only scenes with det_bounded (xrt_api.cpp:
+// |det| < 2^120) reach this test, where a finite det is either < kEPSILON — rejected, so
+// invDet does not matter — or inside rcp_newton's exhaustively checked exact range, and a
+// NaN det gives NaN both ways.
 __device__ __forceinline__ bool ray_tri_nb(v3 o, v3 d, v3 v0, v3 e1, v3 e2, float& t) {
     const v3 pvec = cross(d, e2);
     const float det = dot(e1, pvec);
-    const float invDet = rcp_rn(det);   // == 1.0f / det
+    const float invDet = rcp_newton(det);   // == 1.0f / det wherever it matters
     const v3 tvec = o - v0;
     const float u = dot(tvec, pvec) * invDet;
     const v3 qvec = cross(tvec, e1);
@@ -877,7 +881,7 @@ hipError_t launch_refill(const KParams& P, const uint32_t* count, uint32_t* zero
 
 // ------------------------------------------------------------------- host side ----
 bool use_step_merged(const KParams& P) {
-    return P.scene_kind == SCN_TRI && P.small_tri && P.n_objs <= kMergedMaxObjs && P.n_lights <= kMaxLights &&
+    return P.scene_kind == SCN_TRI && P.small_tri && P.det_bounded && P.n_objs <= kMergedMaxObjs && P.n_lights <= kMaxLights &&
            (P.integrator == XRT_INTEGRATOR_DIRECT || (P.integrator == XRT_INTEGRATOR_GI && P.max_depth > 0)) &&
            !exp_env("XRT_NO_MERGED") && step_merged_lds_bytes(P) <= kStepLds;
 }

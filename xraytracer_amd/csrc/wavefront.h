@@ -191,6 +191,7 @@ struct KParams {
     const int* sbk;           // per ssph entry: original sphere index | (occluder << 30)
     int n_snode;
     int n_segs, n_lights, n_tris, n_sph, n_box, scene_kind, n_objs, small_tri;
+    int det_bounded;   // every triangle has |e1| |e2| < 2^120 (ray_tri_nb's Newton reciprocal, xrt_api.cpp)
     DMedium medium;
     // ---- camera (row-major c2w) + PinholeCamera scale / aspect
     float c2w[16];

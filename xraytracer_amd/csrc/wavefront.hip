@@ -2716,7 +2716,11 @@ hipError_t launch_query(const KParams& P, const float* rays, const float* tmax, 
     const uint32_t blocks = (P.n_slots + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(k_query_in, dim3(blocks), dim3(kBlock), 0, st, P, rays, tmax, mode, list, count);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = launch_trace(P, list, count, zero, blocks, st);
+    // the caller's directions need not be unit vectors, so |det| is not bounded by det_bounded's
+    // |e1| |e2|: phase A takes the per-lane test (IEEE-exact reciprocal) instead of the pair passes
+    KParams Q = P;
+    Q.sstep = nullptr;
+    if (e == hipSuccess) e = launch_trace(Q, list, count, zero, blocks, st);
     if (e != hipSuccess) return e;
     switch (P.scene_kind) {
         case SCN_TRI: hipLaunchKernelGGL(k_query_out<SCN_TRI>, dim3(blocks), dim3(kBlock), 0, st, P, mode, out); break;

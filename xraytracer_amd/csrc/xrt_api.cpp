@@ -261,6 +261,7 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
     auto V = [](const float* p) { return Vec3f(p[0], p[1], p[2]); };
     auto F4 = [](const Vec3f& v, float w) { return f4{v[0], v[1], v[2], w}; };
     auto bits = [](int x) { float f; std::memcpy(&f, &x, 4); return f; };
+    double emax = 0.0;   // largest |e1| |e2| of a triangle (bounds |det| of every ray test)
     for (uint32_t k = 0; k < s->n_objects; ++k) {
         const xrt_object& o = s->objects[k];
         if (o.light >= (int)s->n_lights || o.count < 0 || o.first < 0)
@@ -285,6 +286,7 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
                 const float* n = s->tri_n + 9 * (size_t)t;
                 const Vec3f v0 = V(v), v1 = V(v + 3), v2 = V(v + 6);
                 const Vec3f e1 = v1 - v0, e2 = v2 - v0;     // Src/primitive.cpp:142-143
+                emax = std::max(emax, std::sqrt((double)dot(e1, e1) * (double)dot(e2, e2)));
                 for (int a = 0; a < 3; ++a)
                     if (!(v[a] == vfirst[a] && v[3 + a] == vfirst[a] && v[6 + a] == vfirst[a]) ||
                         !plane_tri_ok(e1.getPtr(), e2.getPtr(), a))
@@ -373,6 +375,10 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
     // Moller-Trumbore hit position, so culling never removes a hit the linear scan accepts.
     P.small_tri = 0;
     P.n_objs = (int)objs.size();
+    // |det| = |e1 . (d x e2)| <= |e1| |e2| |d| with |d| = 1 (+ a few ulp) for every traced ray,
+    // so below 2^120 every finite det is either < kEPSILON (rejected whatever 1/det is) or in
+    // rcp_newton's exact range: ray_tri_nb then skips the IEEE fallback (det_bounded).
+    P.det_bounded = emax < 0x1p120 ? 1 : 0;   // NaN / inf edges: false
     if (P.scene_kind == SCN_TRI && P.n_tris <= kSmallTris && P.n_objs <= kSmallObjs && P.n_tris > 0) {
         float lo[3] = {3e38f, 3e38f, 3e38f}, hi[3] = {-3e38f, -3e38f, -3e38f};
         std::vector<DObjBox> boxes(objs.size());
@@ -497,7 +503,7 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
             P.n_stri = (int)(stri.size() / 3), P.n_sobj = (int)sboxes.size(), P.two_level = 1;
             if (sboxes.size() <= (size_t)kMergedMaxObjs) {   // phase A as cooperative pair passes
                 build_step_objs(sboxes.data(), splanes.data(), (int)sboxes.size(), c->sstep);
-                P.sstep = &c->sstep;
+                P.sstep = P.det_bounded ? &c->sstep : nullptr;   // k_trace_2a_coop: ray_tri_nb
             }
         }
         const BvhBuild B = build_bvh(mn.data(), mx.data(), (uint32_t)nt, kBvhLeaf, 1e-4f * diag + 1e-4f, kBvhMaxDepth);
