@@ -122,14 +122,12 @@ def main():
     fb = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
     timing = not args.no_timing
 
+    sharded = distributed.ShardedRenderer(r, dist)
+
     def step(timed):
-        # the render waits for the work queued on torch's stream (the previous step's reduce)
-        # before it overwrites fb (xrt_render_device_after)
-        st = r.render_device(scene, W, H, fb.data_ptr(), shard_index=rank, shard_count=world,
-                             timing=timing and timed, schedule=args.schedule,
-                             after_stream=torch.cuda.current_stream(dev).cuda_stream)
-        distributed.reduce_framebuffer(fb, dist)
-        return st
+        # rank's rows, then reduce(SUM) into rank 0; the render waits for the work queued on
+        # torch's stream (the previous step's reduce) before it overwrites fb
+        return sharded.render(scene, W, H, fb, timing=timing and timed, schedule=args.schedule)
 
     for _ in range(args.warmup):
         step(False)
@@ -155,10 +153,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist is not None:
         elapsed = distributed.max_over_ranks(elapsed, dist, device=dev)
-        tot = torch.tensor([agg["segments"], agg["shadow_rays"], agg["draws"], agg["samples"]],
-                           dtype=torch.float64, device=dev)
-        dist.all_reduce(tot)
-        agg["segments"], agg["shadow_rays"], agg["draws"], agg["samples"] = [float(x) for x in tot.tolist()]
+        agg = distributed.sum_counters(agg, dist, device=dev)
 
     if rank == 0:
         total_samples = W * H * SPP * args.steps

@@ -6,6 +6,7 @@ by tests/test_gpu_parity.py::test_shards_reassemble_exactly) into a zero framebu
 xraytracer_amd.distributed.reduce_framebuffer sums them to rank 0.  The assembled image
 must equal the single-process render bit for bit.
 """
+import ctypes
 import os
 import socket
 
@@ -59,3 +60,74 @@ def test_row_shards_reduce_to_full_image(tmp_path, world):
     got = np.load(out)
     full, _ = pyoracle.render(scenes.cornell(W, H), W, H, SPP, nthreads=1)
     assert np.array_equal(got, full)
+
+
+class _OracleShardRenderer:
+    """Stand-in for HipRenderer.render_device on CPU: writes the oracle's shard into the
+    framebuffer's memory through the pointer, as the library writes a device buffer."""
+
+    def __init__(self, spp):
+        self.spp = spp
+        self.calls = []
+
+    def render_device(self, scene, width, height, out_ptr, shard_index=0, shard_count=1, after_stream=None, **kw):
+        import pyoracle
+        part, _ = pyoracle.render(scene, width, height, self.spp, nthreads=1, shard_index=shard_index,
+                                  shard_count=shard_count)
+        part = np.ascontiguousarray(part, dtype=np.float32)
+        ctypes.memmove(out_ptr, part.ctypes.data, part.nbytes)
+        self.calls.append((shard_index, shard_count, after_stream))
+        return {"samples": width * len(range(shard_index, height, shard_count)) * self.spp}
+
+
+def _sharded_worker(rank, world, port, out_path, steps):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    from xraytracer_amd import distributed, scenes
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    s = scenes.cornell(W, H)
+    r = _OracleShardRenderer(SPP)
+    sr = distributed.ShardedRenderer(r, dist)
+    assert sr.rows(H) == distributed.shard_rows(H, rank, world)
+    fb = torch.full((H, W, 3), 7.0)   # stale contents: every step overwrites the whole buffer
+    frames = []
+    for _ in range(steps):
+        st = sr.render(s, W, H, fb)
+        if rank == 0:
+            frames.append(fb.numpy().copy())
+    assert r.calls == [(rank, world, None)] * steps
+    tot = distributed.sum_counters({"samples": st["samples"], "iterations": 5}, dist)
+    assert tot["samples"] == W * H * SPP and tot["iterations"] == 5
+    if rank == 0:
+        np.save(out_path, np.stack(frames))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_renderer_every_step_exact(tmp_path, world):
+    """ShardedRenderer (bench.py's step): several frames in a row into the same buffer, each
+    assembled on rank 0 equal to the one-process render; world 3 leaves uneven row counts."""
+    import pyoracle
+    from xraytracer_amd import scenes
+    out = str(tmp_path / "frames.npy")
+    mp.spawn(_sharded_worker, args=(world, _free_port(), out, 3), nprocs=world, join=True)
+    got = np.load(out)
+    full, _ = pyoracle.render(scenes.cornell(W, H), W, H, SPP, nthreads=1)
+    assert got.shape[0] == 3
+    for f in got:
+        assert np.array_equal(f, full)
+
+
+def test_sharded_renderer_rejects_bad_buffer():
+    from xraytracer_amd import distributed
+    sr = distributed.ShardedRenderer(_OracleShardRenderer(1), None)
+    assert (sr.rank, sr.world) == (0, 1)
+    with pytest.raises(ValueError):
+        sr.render(None, W, H, torch.zeros((H, W + 1, 3)))
+    with pytest.raises(ValueError):
+        distributed.ShardedRenderer(_OracleShardRenderer(1), None, dst=1)

@@ -6,8 +6,18 @@ image.  Pixels are independent in the reference (per-pixel seed j + width*i, per
 accumulation: Src/renderer.cpp:35-36, 75), so the sum is exact: every pixel receives one
 rank's value plus zeros.  On ROCm the "nccl" backend is RCCL over xGMI; the tests use
 "gloo" on CPU.
+
+``ShardedRenderer`` is the torchrun-side counterpart of the reference's ParallelRenderer
+(Src/renderer.cpp:83-99, a thread pool over the rows of one machine): the same row split,
+one process per GPU instead of one thread per row, and the frame assembled by a collective
+instead of shared memory.  C/C++ callers get the same split inside the library
+(``xrt_create_multi``; ``HipRenderer(spp, cam, integ, devices)``).
 """
 from __future__ import annotations
+
+# counters of XrtStats that are per-rank work and sum over ranks (the rest are per-rank
+# launch statistics: schedule, iterations, kernel times)
+SUMMED_COUNTERS = ("segments", "shadow_rays", "draws", "samples", "rejected")
 
 
 def shard_rows(height: int, rank: int, world: int):
@@ -15,9 +25,19 @@ def shard_rows(height: int, rank: int, world: int):
     return list(range(rank, height, world))
 
 
+def _world(dist):
+    if dist is None or not dist.is_initialized():
+        return 0, 1
+    return dist.get_rank(), dist.get_world_size()
+
+
 def reduce_framebuffer(fb, dist, dst: int = 0):
-    """Sum the per-rank framebuffers into rank `dst` (in place)."""
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    """Sum the per-rank framebuffers into rank `dst` (in place).
+
+    With async_op=False torch makes the caller's current stream wait for the collective, so
+    a later render that waits on that stream (xrt_render_device_after) cannot overwrite `fb`
+    while the reduce still reads it."""
+    if _world(dist)[1] == 1:
         return fb
     dist.reduce(fb, dst=dst, op=dist.ReduceOp.SUM)
     return fb
@@ -25,9 +45,53 @@ def reduce_framebuffer(fb, dist, dst: int = 0):
 
 def max_over_ranks(value: float, dist, device=None) -> float:
     """Slowest rank's time (the bench reports whole-job throughput against it)."""
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    if _world(dist)[1] == 1:
         return value
     import torch
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def sum_counters(counters: dict, dist, device=None) -> dict:
+    """Whole-job totals of the SUMMED_COUNTERS present in `counters` (other keys unchanged)."""
+    out = dict(counters)
+    if _world(dist)[1] == 1:
+        return out
+    import torch
+    keys = [k for k in SUMMED_COUNTERS if k in counters]
+    t = torch.tensor([float(counters[k]) for k in keys], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    out.update(zip(keys, t.tolist()))
+    return out
+
+
+class ShardedRenderer:
+    """One rank's share of a frame rendered by every rank of `dist` (ParallelRenderer shape).
+
+    renderer: anything with HipRenderer.render_device's signature (one GPU per rank).
+    render(scene, W, H, fb) renders this rank's rows into the device tensor `fb` (H, W, 3)
+    float32 — zeros elsewhere — after the work already queued on torch's current stream,
+    then reduces the frame into rank `dst`.  Only rank `dst`'s `fb` holds the image."""
+
+    def __init__(self, renderer, dist=None, dst: int = 0):
+        self.renderer = renderer
+        self.dist = dist
+        self.dst = dst
+        self.rank, self.world = _world(dist)
+        if not 0 <= dst < self.world:
+            raise ValueError(f"dst rank {dst} outside world of {self.world}")
+
+    def rows(self, height: int):
+        return shard_rows(height, self.rank, self.world)
+
+    def render(self, scene, width: int, height: int, fb, after_stream=None, **kw):
+        if tuple(fb.shape) != (height, width, 3) or not fb.is_contiguous():
+            raise ValueError(f"framebuffer must be a contiguous ({height}, {width}, 3) tensor, got {tuple(fb.shape)}")
+        import torch
+        if after_stream is None and fb.is_cuda:
+            after_stream = torch.cuda.current_stream(fb.device).cuda_stream
+        st = self.renderer.render_device(scene, width, height, fb.data_ptr(), shard_index=self.rank,
+                                         shard_count=self.world, after_stream=after_stream, **kw)
+        reduce_framebuffer(fb, self.dist, self.dst)
+        return st
