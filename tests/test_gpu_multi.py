@@ -78,3 +78,29 @@ def test_cpp_multi_gpu_renderer(tmp_path):
     img = np.fromfile(out, dtype=np.float32).reshape(48, 64, 3)
     ref, _ = pyoracle.render(scenes.cornell(64, 48), 64, 48, 4)
     assert np.array_equal(img, ref)
+
+
+def test_sharded_renderer_device_frames(single):
+    """bench.py's step on one GPU: distributed.ShardedRenderer over HipRenderer.render_device
+    into one torch tensor, frame after frame (the render waits on torch's current stream, so
+    a stale buffer and queued torch work are overwritten in order), each frame equal to the
+    oracle; a row shard of the same tensor holds the oracle's shard rows and zeros."""
+    import torch
+    from xraytracer_amd import distributed
+
+    W, H = 72, 40
+    s = scenes.cornell(W, H)
+    single.spp = 4
+    sr = distributed.ShardedRenderer(single, None)
+    fb = torch.full((H, W, 3), 3.0, dtype=torch.float32, device="cuda:0")
+    ref, st = pyoracle.render(s, W, H, 4)
+    for _ in range(2):
+        fb.mul_(2.0)   # torch work queued on the current stream before the render
+        got = sr.render(s, W, H, fb)
+        assert np.array_equal(fb.cpu().numpy(), ref)
+        assert (got.samples, got.segments, got.draws) == (W * H * 4, st["segments"], st["draws"])
+    part, _ = pyoracle.render(s, W, H, 4, shard_index=1, shard_count=3)
+    got = single.render_device(s, W, H, fb.data_ptr(), shard_index=1, shard_count=3,
+                               after_stream=torch.cuda.current_stream().cuda_stream)
+    assert np.array_equal(fb.cpu().numpy(), part)
+    assert got.samples == W * len(distributed.shard_rows(H, 1, 3)) * 4
