@@ -56,7 +56,14 @@ def cpu_quota():
         return None
 
 
-def cpu_baseline(cfg_name, cfg, spp):
+# Bounded CPU sample per workload (about 10-20 s of the oracle on the box's 16 CPUs): rows
+# y % shard_count == 0 of the workload's own image at `spp` samples per pixel.  The oracle
+# restates the reference's linear scans (no acceleration structure), so C3's 1,001 spheres
+# and C4's 51,236 triangles cost far more per sample than C2's 36 triangles.
+CPU_SAMPLE = {"C1": (1, 256), "C2": (1, 256), "C3": (16, 96), "C4": (256, 2), "C5": (1, 128)}
+
+
+def cpu_baseline(cfg_name, cfg, spp=None):
     """The oracle (CPU restatement, bit-exact with the GPU path) on every CPU this process
     may use: one OpenMP thread per CPU of os.sched_getaffinity, or per CPU of the cgroup's
     CPU quota when that is smaller (more threads than the quota only time-slice: measured
@@ -67,16 +74,41 @@ def cpu_baseline(cfg_name, cfg, spp):
     affinity = max(1, len(os.sched_getaffinity(0)))
     quota = cpu_quota()
     threads = affinity if not quota else max(1, min(affinity, int(quota + 0.5)))
+    shards, dspp = CPU_SAMPLE.get(cfg_name, (1, 256))
+    spp = spp or dspp
     s = scenes.build(cfg_name)
     w, h = cfg["width"], cfg["height"]
     t0 = time.perf_counter()
-    _, st = pyoracle.render(s, w, h, spp, nthreads=threads)
+    _, st = pyoracle.render(s, w, h, spp, nthreads=threads, shard_index=0, shard_count=shards)
     dt = time.perf_counter() - t0
-    return {"value": round(w * h * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{cfg_name} scene {w}x{h} at {spp} spp (cost is linear in spp), oracle/oracle.c "
-                      f"with OpenMP over rows, {threads} threads = every CPU this process may use "
-                      f"({affinity} in its affinity mask"
+    rows = len(range(0, h, shards))
+    what = f"rows y % {shards} == 0 ({rows} of {h}) of " if shards > 1 else ""
+    return {"value": round(st["samples"] / dt / 1e6, 6), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{what}{cfg_name} scene {w}x{h} at {spp} spp ({st['samples']} samples; cost is linear in "
+                      f"spp), oracle/oracle.c (the reference's linear scans) with OpenMP over rows, {threads} threads "
+                      f"= every CPU this process may use ({affinity} in its affinity mask"
                       + (f", cgroup CPU quota {quota:g}" if quota else "") + f"), {dt:.2f} s wall"}
+
+
+def hip_kernel_name(kid, sched, scene):
+    """The HIP kernel behind an xrt_stats kernel family for this schedule / scene (the name
+    rocprofv3 reports, which the PMC summaries are keyed by)."""
+    from xraytracer_amd import abi
+    if kid == abi.XRT_K_STEP:
+        return "k_" + abi.SCHEDULE_NAMES[sched] if sched in (abi.XRT_SCHED_STEP_TRI, abi.XRT_SCHED_STEP_MERGED) \
+            else "k_step"
+    if kid == abi.XRT_K_TRACE and scene.desc.n_tris > 1024:   # two-level trace: phase A
+        return "k_trace_2a_coop"
+    return "k_" + abi.KERNEL_NAMES[kid]
+
+
+def load_keyed(path, cfg, kernel):
+    """A PMC / traffic summary (tools/prof_summary.py) if it is for this config and kernel."""
+    try:
+        j = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    return j if j.get("config") == cfg and j.get("kernel") == kernel else None
 
 
 def main():
@@ -87,12 +119,14 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--spp", type=int, default=None, help="override spp (never for reported numbers)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-spp", type=int, default=256)
+    ap.add_argument("--cpu-spp", type=int, default=None, help="override the CPU sample's spp")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--schedule", default="auto", choices=("auto", "wavefront"))
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--traffic", default=None, help="default profiles/traffic_<CONFIG>.json")
+    ap.add_argument("--pmc", default=None, help="default profiles/pmc_<CONFIG>.json")
     args = ap.parse_args()
+    args.traffic = args.traffic or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    args.pmc = args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
 
     import numpy as np
     import torch
@@ -166,44 +200,33 @@ def main():
             q = agg["segments"] / max(1, agg["samples"])
             dpp = agg["draws"] / max(1, agg["samples"])
             b_s = B_SAMPLE + B_SEGMENT * q + B_DRAW * dpp
-            dom = max((abi.XRT_K_TRACE, abi.XRT_K_SHADE, abi.XRT_K_STEP), key=lambda k: kms[k])
+            dom = max((abi.XRT_K_TRACE, abi.XRT_K_SHADE, abi.XRT_K_STEP, abi.XRT_K_DEEP), key=lambda k: kms[k])
             if dom == abi.XRT_K_STEP:
                 kbytes = b_s * samples
             elif dom == abi.XRT_K_TRACE:
                 kbytes = B_TRACE_SEG * q * samples
-            else:
+            elif dom == abi.XRT_K_SHADE:
                 kbytes = (b_s - B_TRACE_SEG * q) * samples
+            else:   # the deep BVH walk: only its queued rays' share of the trace is known per ray
+                kbytes = None
             launches = max(1, kl[dom])
-            per_launch = kbytes / launches
             avg_s = kms[dom] / 1e3 / launches
-            achieved = per_launch / avg_s / 1e9
-            kname = abi.KERNEL_NAMES[dom]
-            if dom == abi.XRT_K_STEP and sched in (abi.XRT_SCHED_STEP_TRI, abi.XRT_SCHED_STEP_MERGED):
-                kname = abi.SCHEDULE_NAMES[sched]   # k_step_tri / k_step_merged
-            traffic = None
-            if os.path.exists(args.traffic):
-                try:
-                    tj = json.load(open(args.traffic))
-                    if tj.get("config") == args.config and tj.get("kernel") == "k_" + kname:
-                        traffic = tj.get("hbm_bytes_per_launch")
-                except (OSError, ValueError):
-                    traffic = None
-            # measured limiter, from the PMC passes of the same kernel and workload
-            # (tools/profile.sh -> tools/prof_summary.py -> profiles/pmc_latest.json):
+            kname = hip_kernel_name(dom, sched, scene)
+            # measured traffic and limiter, from the PMC passes of the same kernel and workload
+            # (tools/evidence.sh CONFIG -> tools/prof_summary.py -> profiles/{pmc,traffic}_CONFIG.json):
             #   VALU issue: SQ_INSTS_VALU per launch / avg launch time vs VALU_PEAK_GINST
             #   HBM:        (FETCH_SIZE x2 + WRITE_SIZE) per launch / avg launch time vs 8 TB/s
-            pmc = None
-            if os.path.exists(args.pmc):
-                try:
-                    pj = json.load(open(args.pmc))
-                    if pj.get("config") == args.config and pj.get("kernel") == "k_" + kname:
-                        pmc = pj
-                except (OSError, ValueError):
-                    pmc = None
-            model = {"what": "SURVEY.md 8d algorithmic bytes, B_s = 68 + 264*Q + 12*D per sample",
-                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "bytes_per_sample": round(b_s, 2),
-                     "algorithmic_bytes_per_launch": round(per_launch, 1)}
+            tj = load_keyed(args.traffic, args.config, kname)
+            traffic = tj.get("hbm_bytes_per_launch") if tj else None
+            pmc = load_keyed(args.pmc, args.config, kname)
+            model = None
+            if kbytes is not None:
+                per_launch = kbytes / launches
+                achieved = per_launch / avg_s / 1e9
+                model = {"what": "SURVEY.md 8d algorithmic bytes, B_s = 68 + 264*Q + 12*D per sample",
+                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "bytes_per_sample": round(b_s, 2),
+                         "algorithmic_bytes_per_launch": round(per_launch, 1)}
             hbm = None
             if traffic:
                 hbm = {"achieved": round(traffic / avg_s / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -222,10 +245,13 @@ def main():
                 head, bound = valu, "valu"
             elif hbm:
                 head, bound = hbm, "hbm"
-            else:   # no counters for this build: the model figure, labelled as such
+            elif model:   # no counters for this build: the model figure, labelled as such
                 head, bound = model, "hbm (model; unmeasured)"
-            roof = {"bound": bound, "kernel": "k_" + kname, "achieved": head["achieved"], "peak": head["peak"],
+            else:
+                head, bound = {"achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None}, "unmeasured"
+            roof = {"bound": bound, "kernel": kname, "achieved": head["achieved"], "peak": head["peak"],
                     "unit": head["unit"], "frac": head["frac"], "traffic": traffic,
+                    "traffic_source": (tj or {}).get("source"),
                     "avg_launch_us": round(avg_s * 1e6, 3), "launches": int(kl[dom]),
                     "valu_issue": valu, "hbm_measured": hbm, "model": model,
                     "pmc_source": (pmc or {}).get("source")}

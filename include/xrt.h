@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 8
+#define XRT_ABI_VERSION 9
 
 /* ---- status codes ---------------------------------------------------------------- */
 enum {
@@ -153,9 +153,11 @@ typedef struct {
     uint32_t visits_per_launch; /* 0 or 1..128 path segments per slot per step launch    */
 } xrt_render_params;
 
+/* kernel families timed in xrt_stats: XRT_K_TRACE is the wavefront trace (for two-level
+ * scenes its phase A, the small objects), XRT_K_DEEP the BVH walk of the rays phase A queued */
 enum {
     XRT_K_SEED = 0, XRT_K_TRACE = 1, XRT_K_SHADE = 2, XRT_K_FINISH = 3, XRT_K_STEP = 4, XRT_K_REFILL = 5,
-    XRT_K_COUNT = 6
+    XRT_K_DEEP = 6, XRT_K_COUNT = 7
 };
 
 /* device schedules: multi-pass wavefront (k_shade + k_trace), fused per-slot k_step with
@@ -181,6 +183,9 @@ typedef struct {
     uint32_t group_lanes;        /* lanes sharing one slot's traces (1 = pair passes)      */
     uint32_t partitions;         /* live-list partitions                                   */
     uint32_t visits_per_launch;  /* path segments per slot per step launch                 */
+    uint64_t rng_twists;         /* mt19937 blocks generated (624 words each) over all slots,
+                                    including each slot's first: rng_twists - path_slots is
+                                    the number of ring refills done while paths were live  */
 } xrt_stats;
 
 /* ---- context ----------------------------------------------------------------------- */

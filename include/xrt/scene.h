@@ -5,6 +5,7 @@
 // produces the C-ABI description uploaded by HipRenderer.
 #pragma once
 #include <memory>
+#include <filesystem>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -24,8 +25,10 @@ public:
     Scene(const Scene&) = delete;
     Scene& operator=(const Scene&) = delete;
     // Scene::loadObj (Src/scene.cpp:46-154) with tinyobjloader v2 parsing/triangulation;
-    // returns false (and sets lastError) where the reference calls exit(1).
-    bool loadObj(const std::string& filepath);
+    // same parameter as the reference (a std::string converts implicitly); returns false
+    // (and sets lastError) where the reference calls exit(1) — callers that ignore the
+    // result, as the reference's examples do, compile unchanged.
+    bool loadObj(const std::filesystem::path& filepath);
     void addObj(std::string name, std::unique_ptr<Object> obj);
     void build() {}
     void addAreaLight(std::string name, std::unique_ptr<AreaLight> light);
@@ -33,10 +36,10 @@ public:
     // uniform choice among the area lights (Src/scene.cpp:182-188): one draw
     const AreaLight* sampleAreaLight(Sampler& sampler, float& pdf) const;
     // Scene::intersect / Scene::occluded (Src/scene.cpp:190-211), answered on the GPU by
-    // the renderer's own trace kernels (xrt_query on a context of device 0, created and
-    // uploaded on first use and after the scene changes).  `info` must be fresh (t = t1 =
-    // kInfinity), as at every call site of the reference; on a device error intersect /
-    // occluded return false and lastError() says why.
+    // the renderer's own trace kernels (xrt_query on a context of queryDevice(), created and
+    // uploaded on first use and re-uploaded after addObj / loadObj / markChanged).  `info`
+    // must be fresh (t = t1 = kInfinity), as at every call site of the reference; on a device
+    // error intersect / occluded return false and lastError() says why.
     bool intersect(const Ray& ray, IntersectInfo& info) const;
     bool occluded(const Ray& ray, float t_max) const;
     // batched forms: one GPU pass for all rays
@@ -44,6 +47,13 @@ public:
     void occluded(const std::vector<Ray>& rays, const std::vector<float>& t_max, std::vector<char>& hits) const;
 
     // ---- additions for the GPU backend ----
+    // HIP device that answers intersect / occluded (default 0).  Changing it drops the
+    // current query context; the next query re-creates and re-uploads on the new device.
+    void setQueryDevice(int device);
+    int queryDevice() const { return m_qdevice; }
+    // Geometry edited in place through an object pointer (not via addObj / loadObj) is not
+    // seen by the query context until the scene is marked changed.
+    void markChanged() { ++m_version; }
     // Flattened, in m_objects iteration order; valid until the scene changes.
     int flatten(xrt_scene_desc* out) const;
     // the one medium referenced by objects (VolumePathTracing scenes), or nullptr;
@@ -65,6 +75,7 @@ private:
     uint64_t m_version = 0;
     mutable uint64_t m_qversion = ~0ull;
     mutable xrt_ctx* m_qctx = nullptr;
+    int m_qdevice = 0;
     mutable std::vector<const Object*> m_order;
     bool query(const float* rays, const float* tmax, uint32_t n, int mode, xrt_hit* out) const;
     void fillInfo(const xrt_hit& h, IntersectInfo& info) const;

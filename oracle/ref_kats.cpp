@@ -347,6 +347,58 @@ int main() {
         o.key("bxdf_eval"); o.arr(ev);
     }
 
+    // 10. Host-side geometry of the drop-in API (include/xrt/geometry.h): Matrix44f::inverse
+    //     (Gauss-Jordan, Src/geometry.h:509-590), operator* and transposed (:314-425) on the
+    //     cameras above, random affine and random dense matrices and one singular matrix;
+    //     worldToLocal / localToWorld (:686-701) in frames from orthonormalBasis.
+    {
+        Gen g(0xC0FFEEu);
+        std::vector<Matrix44f> ms = {Matrix44f(-1.0, 0, 0, 0, 0, 1.0, 0, 0, 0, 0, -1.0, 0, 278, 274.4, -750.0, 1),
+                                     Matrix44f(1, 2, 3, 4, 2, 4, 6, 8, 0, 1, 0, 0, 0, 0, 1, 1)};   // singular
+        for (int k = 0; k < 40; ++k) {
+            Matrix44f m;
+            const bool affine = k < 20;
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j) m[i][j] = (affine && j == 3) ? (i == 3 ? 1.0f : 0.0f) : g.uni(-2.0f, 2.0f);
+            if (affine)
+                for (int j = 0; j < 3; ++j) m[3][j] = g.uni(-500.0f, 500.0f);
+            ms.push_back(m);
+        }
+        std::vector<uint32_t> mats, inv, prod, tr;
+        for (size_t q = 0; q < ms.size(); ++q) {
+            const Matrix44f& m = ms[q];
+            const Matrix44f& n = ms[(q + 1) % ms.size()];
+            const Matrix44f mi = m.inverse(), mn = m * n, mt = m.transposed();
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j) {
+                    mats.push_back(bits(m[i][j]));
+                    inv.push_back(bits(mi[i][j]));
+                    prod.push_back(bits(mn[i][j]));
+                    tr.push_back(bits(mt[i][j]));
+                }
+        }
+        o.key("m44_in"); o.arr(mats);
+        o.key("m44_inverse"); o.arr(inv);
+        o.key("m44_mul_next"); o.arr(prod);
+        o.key("m44_transposed"); o.arr(tr);
+        std::vector<uint32_t> in, w2l, l2w;
+        for (int k = 0; k < 256; ++k) {
+            const Vec3f n = normalize(g.vec(-1.0f, 1.0f));
+            Vec3f t, b;
+            orthonormalBasis(n, t, b);
+            const Vec3f v = g.vec(-3.0f, 3.0f);
+            push3(in, v);
+            push3(in, t);
+            push3(in, n);
+            push3(in, b);
+            push3(w2l, worldToLocal(v, t, n, b));
+            push3(l2w, localToWorld(v, t, n, b));
+        }
+        o.key("frame_in"); o.arr(in);
+        o.key("frame_w2l"); o.arr(w2l);
+        o.key("frame_l2w"); o.arr(l2w);
+    }
+
     o.s += "\n}\n";
     std::fputs(o.s.c_str(), stdout);
     return 0;

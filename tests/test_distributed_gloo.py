@@ -131,3 +131,6 @@ def test_sharded_renderer_rejects_bad_buffer():
         sr.render(None, W, H, torch.zeros((H, W + 1, 3)))
     with pytest.raises(ValueError):
         distributed.ShardedRenderer(_OracleShardRenderer(1), None, dst=1)
+    # row shards + SUM reduce cannot accumulate in place
+    with pytest.raises(ValueError):
+        sr.render(None, W, H, torch.zeros((H, W, 3)), accumulate=True)

@@ -104,3 +104,69 @@ def test_sharded_renderer_device_frames(single):
                                after_stream=torch.cuda.current_stream().cuda_stream)
     assert np.array_equal(fb.cpu().numpy(), part)
     assert got.samples == W * len(distributed.shard_rows(H, 1, 3)) * 4
+
+
+def _slow_then_fill(stream, fb, value):
+    """Queue ~tens of ms of GPU work on `stream`, then overwrite fb: a render that does not
+    wait for `stream` would run before the fill and be clobbered by it."""
+    import torch
+
+    with torch.cuda.stream(stream):
+        if hasattr(torch.cuda, "_sleep"):
+            torch.cuda._sleep(50_000_000)
+        else:   # pragma: no cover - older torch
+            x = torch.randn(4096, 4096, device=fb.device)
+            for _ in range(8):
+                x = x @ x
+                x = x / x.norm()
+        fb.fill_(value)
+
+
+@pytest.mark.parametrize("which", ["side", "legacy_null"])
+def test_sharded_render_waits_for_long_work_on_after_stream(single, which):
+    """ShardedRenderer's render must start only after the work queued on
+    the stream it is given.  Long work (a device sleep) followed by a fill of the framebuffer
+    is queued on a side stream (or the legacy null stream, handle 0); the render is told to
+    wait on that stream and must still produce the oracle's image, not the fill value."""
+    import torch
+    from xraytracer_amd import distributed
+
+    W, H = 64, 40
+    s = scenes.cornell(W, H)
+    single.spp = 3
+    ref, _ = pyoracle.render(s, W, H, 3)
+    sr = distributed.ShardedRenderer(single, None)
+    fb = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0")
+    torch.cuda.synchronize()
+    if which == "side":
+        stream = torch.cuda.Stream(device="cuda:0")
+        handle = stream.cuda_stream
+    else:
+        stream = torch.cuda.default_stream("cuda:0")
+        handle = 0
+        assert stream.cuda_stream == 0
+    for _ in range(2):
+        _slow_then_fill(stream, fb, 9.0)
+        sr.render(s, W, H, fb, after_stream=handle)
+        torch.cuda.synchronize()
+        assert np.array_equal(fb.cpu().numpy(), ref)
+    if which == "side":
+        # control: told to wait on an idle stream, the render finishes first and the queued
+        # fill lands on top of it — so the queued work above was long enough to matter
+        idle = torch.cuda.Stream(device="cuda:0")
+        _slow_then_fill(stream, fb, 9.0)
+        sr.render(s, W, H, fb, after_stream=idle.cuda_stream)
+        torch.cuda.synchronize()
+        assert np.all(fb.cpu().numpy() == 9.0)
+
+
+def test_sharded_render_rejects_accumulate(single):
+    """row shards + a SUM reduce cannot accumulate (each rank's unowned rows would
+    be added once per rank), so ShardedRenderer refuses accumulate=True."""
+    import torch
+    from xraytracer_amd import distributed
+
+    sr = distributed.ShardedRenderer(single, None)
+    fb = torch.zeros((8, 8, 3), dtype=torch.float32, device="cuda:0")
+    with pytest.raises(ValueError):
+        sr.render(scenes.cornell(8, 8), 8, 8, fb, accumulate=True)

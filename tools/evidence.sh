@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/evidence.sh TAG [CONFIG] — the measurement evidence of a round, on the GPU box:
 #   1. rocprofv3 kernel-trace/stats + PMC passes of bench.py (tools/profile.sh)
-#   2. per-launch HBM traffic of the dominant kernel -> profiles/traffic_latest.json
+#   2. per-launch HBM traffic / SQ counters of the dominant kernel -> profiles/{traffic,pmc}_CONFIG.json
 #   3. the default bench.py line (with the CPU baseline) -> gpurun_out/TAG/bench.json
 # Copy gpurun_out/TAG/{kt_kernel_stats.csv,summary.txt,bench.json} into profiles/ after.
 set -euo pipefail
@@ -16,9 +16,9 @@ import re
 print(re.search(r"(k_\w+)", top["Name"]).group(1))
 PY
 )
-python3 "$R/tools/prof_summary.py" "$R/gpurun_out/$TAG" "$KPAT" --traffic "$CFG" "$R/profiles/traffic_latest.json" \
-    --pmc "$CFG" "$R/profiles/pmc_latest.json" --csv "$R/gpurun_out/$TAG/pmc_dispatch.csv" > "$R/gpurun_out/$TAG/summary.txt"
+python3 "$R/tools/prof_summary.py" "$R/gpurun_out/$TAG" "$KPAT" --traffic "$CFG" "$R/profiles/traffic_$CFG.json" \
+    --pmc "$CFG" "$R/profiles/pmc_$CFG.json" --csv "$R/gpurun_out/$TAG/pmc_dispatch.csv" > "$R/gpurun_out/$TAG/summary.txt"
 cp "$R/gpurun_out/$TAG/kt/kt_kernel_stats.csv" "$R/gpurun_out/$TAG/kt_kernel_stats.csv"
-mkdir -p "$R/gpurun_out/profiles_new" && cp "$R/profiles/traffic_latest.json" "$R/profiles/pmc_latest.json" "$R/gpurun_out/profiles_new/"
+mkdir -p "$R/gpurun_out/profiles_new" && cp "$R/profiles/traffic_$CFG.json" "$R/profiles/pmc_$CFG.json" "$R/gpurun_out/profiles_new/"
 timeout -k 10 600 python3 "$R/bench.py" --config "$CFG" > "$R/gpurun_out/$TAG/bench.json"
 cat "$R/gpurun_out/$TAG/bench.json"

@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(HERE, "libxrt_hip.so")
 if os.environ.get("XRT_LIB"):   # experiment builds (csrc/Makefile `variant`), same ABI
     LIB_PATH = os.path.join(HERE, os.environ["XRT_LIB"])
 
-XRT_ABI_VERSION = 8   # include/xrt.h XRT_ABI_VERSION
+XRT_ABI_VERSION = 9   # include/xrt.h XRT_ABI_VERSION
 XRT_OK = 0
 XRT_OBJ_MESH, XRT_OBJ_SPHERE, XRT_OBJ_BOX = 0, 1, 2
 XRT_LIGHT_QUAD, XRT_LIGHT_TRIANGLE, XRT_LIGHT_SPHERE = 0, 1, 2
@@ -27,8 +27,9 @@ XRT_MEDIUM_HETEROGENEOUS, XRT_MEDIUM_HOMOGENEOUS_MIS, XRT_MEDIUM_HOMOGENEOUS_ACH
 XRT_FLAG_TIMING, XRT_FLAG_WAVEFRONT, XRT_FLAG_NO_MERGED, XRT_FLAG_NO_GROUP, XRT_FLAG_ACCUMULATE = 1, 2, 4, 8, 16
 XRT_SCHED_WAVEFRONT, XRT_SCHED_STEP, XRT_SCHED_STEP_TRI, XRT_SCHED_STEP_MERGED = 0, 1, 2, 3
 SCHEDULE_NAMES = ("wavefront", "step", "step_tri", "step_merged")
-XRT_K_SEED, XRT_K_TRACE, XRT_K_SHADE, XRT_K_FINISH, XRT_K_STEP, XRT_K_REFILL, XRT_K_COUNT = 0, 1, 2, 3, 4, 5, 6
-KERNEL_NAMES = ("seed", "trace", "shade", "finish", "step", "refill")
+XRT_K_SEED, XRT_K_TRACE, XRT_K_SHADE, XRT_K_FINISH, XRT_K_STEP, XRT_K_REFILL, XRT_K_DEEP, XRT_K_COUNT = \
+    0, 1, 2, 3, 4, 5, 6, 7
+KERNEL_NAMES = ("seed", "trace", "shade", "finish", "step", "refill", "trace_deep4")
 
 INTEGRATORS = {"gi": XRT_INTEGRATOR_GI, "direct": XRT_INTEGRATOR_DIRECT, "vpt": XRT_INTEGRATOR_VPT,
                "indirect": XRT_INTEGRATOR_INDIRECT, "normal": XRT_INTEGRATOR_NORMAL, "vpt_nee": XRT_INTEGRATOR_VPT_NEE}
@@ -87,7 +88,8 @@ class XrtStats(C.Structure):
                 ("segments", C.c_uint64), ("shadow_rays", C.c_uint64), ("draws", C.c_uint64),
                 ("rejected", C.c_uint64), ("iterations", C.c_uint64), ("path_slots", C.c_uint64),
                 ("schedule", C.c_uint64), ("stalled", C.c_uint64), ("slots_per_wave", C.c_uint32),
-                ("group_lanes", C.c_uint32), ("partitions", C.c_uint32), ("visits_per_launch", C.c_uint32)]
+                ("group_lanes", C.c_uint32), ("partitions", C.c_uint32), ("visits_per_launch", C.c_uint32),
+                ("rng_twists", C.c_uint64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "launches")}
@@ -160,10 +162,14 @@ def lib():
         # process ("No HIP GPUs are available"; measured on the MI355X box), while the other
         # order works.  Load torch first when it is installed, so callers can render into
         # torch tensors (xrt_render_device) in any import order.
+        # A torch that is installed but broken (its bundled HIP libraries raise OSError /
+        # RuntimeError) must not stop the C path from loading.
         try:
             import torch  # noqa: F401
-        except ImportError:
-            pass
+        except Exception as e:  # noqa: BLE001
+            if not isinstance(e, ImportError):
+                import warnings
+                warnings.warn(f"torch failed to import ({e!r}); loading libxrt_hip without it")
         l = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(l, name)

@@ -436,7 +436,10 @@ int fix_index(int idx, int n, bool& ok) {
 }  // namespace
 
 // Scene::loadObj (Src/scene.cpp:46-154)
-bool Scene::loadObj(const std::string& filepath) {
+bool Scene::loadObj(const std::filesystem::path& path) {
+    // tinyobjloader reads generic_string(); MTL files are looked up next to the OBJ
+    // (reader_config.mtl_search_path = parent_path(), Src/scene.cpp:51-53)
+    const std::string filepath = path.generic_string();
     std::ifstream f(filepath);
     if (!f) {
         m_error = "[Scene] failed to load " + filepath;
@@ -615,10 +618,18 @@ const AreaLight* Scene::sampleAreaLight(Sampler& sampler, float& pdf) const {
     return m_areaLights[lightIdx].get();
 }
 
+void Scene::setQueryDevice(int device) {
+    if (device == m_qdevice) return;
+    if (m_qctx) xrt_destroy(m_qctx);
+    m_qctx = nullptr;
+    m_qversion = ~0ull;
+    m_qdevice = device;
+}
+
 // GPU ray queries (xrt_query): upload on first use and after any change to the objects
 bool Scene::query(const float* rays, const float* tmax, uint32_t n, int mode, xrt_hit* out) const {
     int rc = XRT_OK;
-    if (!m_qctx && (rc = xrt_create(0, &m_qctx)) != XRT_OK) {
+    if (!m_qctx && (rc = xrt_create(m_qdevice, &m_qctx)) != XRT_OK) {
         m_qctx = nullptr;
         m_error = std::string("[Scene] ray query: xrt_create failed: ") + xrt_last_error(nullptr);
         return false;

@@ -24,6 +24,8 @@ hipError_t launch_trace_2a_coop(const KParams& P, const uint32_t* list, const ui
                                 uint32_t blocks, hipStream_t st);
 hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
                         uint32_t blocks, hipStream_t st);
+// phase B of a two-level trace (the BVH walk of the rays launch_trace queued); no-op otherwise
+hipError_t launch_trace_deep(const KParams& P, hipStream_t st);
 hipError_t launch_shade(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
                         uint32_t* out_count, uint32_t* req_count, uint32_t blocks, hipStream_t st);
 // fused schedule (k_step): LDS bytes it needs for this scene, 0 = scene too large for it

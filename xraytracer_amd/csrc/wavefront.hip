@@ -2334,8 +2334,8 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
 // ================================================================== k_finish ====
 // Image::operator/=(Vec3f(n_samples)) over this shard's pixels + counter reduction.
 __global__ __launch_bounds__(kBlock) void k_finish(KParams P) {
-    __shared__ unsigned long long red[5][kBlock / 64];
-    unsigned long long a[5] = {0, 0, 0, 0, 0};
+    __shared__ unsigned long long red[6][kBlock / 64];
+    unsigned long long a[6] = {0, 0, 0, 0, 0, 0};
     const float n = (float)P.spp;
     for (uint32_t s = blockIdx.x * kBlock + threadIdx.x; s < P.n_slots; s += gridDim.x * kBlock) {
         const uint32_t col = s % P.width, row = P.shard_index + P.shard_count * (s / P.width);
@@ -2346,19 +2346,20 @@ __global__ __launch_bounds__(kBlock) void k_finish(KParams P) {
         a[2] += P.rng_c[s] - kMT;
         a[3] += P.c_rej[s];
         a[4] += P.c_stall[s];
+        a[5] += P.rng_g[s] / kMT - 1u;   // twists: k_seed leaves g = kMT, every twist adds kMT
     }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
-    for (int q = 0; q < 5; ++q) {
+    for (int q = 0; q < 6; ++q) {
         unsigned long long v = a[q];
         for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
         if (lane == 0) red[q][wv] = v;
     }
     __syncthreads();
-    if (threadIdx.x < 5) {
+    if (threadIdx.x < 6) {   // stats[0..4], twists to stats[7] (5, 6: experiment counters)
         unsigned long long v = 0;
         for (int w = 0; w < kBlock / 64; ++w) v += red[threadIdx.x][w];
-        atomicAdd(P.stats + threadIdx.x, v);
+        atomicAdd(P.stats + (threadIdx.x < 5 ? threadIdx.x : 7u), v);
     }
 }
 
@@ -2493,6 +2494,22 @@ static hipError_t trace_nl(const KParams& P, const uint32_t* list, const uint32_
     return hipGetLastError();
 }
 
+// Phase B of the two-level trace (P.two_level): the 4-wide BVH walk of the rays phase A
+// queued.  Persistent: up to 2048 blocks (8 per CU), each serving partition blockIdx % n_part.
+// A no-op for every other trace.
+hipError_t launch_trace_deep(const KParams& P, hipStream_t st) {
+    if (!(P.bvh_node && P.scene_kind == SCN_TRI && P.two_level)) return hipSuccess;
+    if (!P.bvh4 || P.bvh4_stack <= 0 || P.bvh4_stack > kBvh4Stack) return hipErrorInvalidValue;
+    const uint32_t db = P.n_part * std::max<uint32_t>(1u, std::min<uint32_t>(2048u / P.n_part,
+                                                                            (P.deep_cap + kBlock - 1) / kBlock));
+    const bool small4 = P.bvh4_nodes <= 0x10000;
+    const size_t ntop4 = std::min<size_t>((size_t)P.bvh4_nodes, kBvhTopNodes);
+    const size_t lds4 = ntop4 * 8 * sizeof(f4) + (size_t)P.bvh4_stack * kBlock * (small4 ? sizeof(uint16_t) : sizeof(uint32_t));
+    if (small4) hipLaunchKernelGGL((k_trace_deep4<uint16_t>), dim3(db), dim3(kBlock), lds4, st, P);
+    else hipLaunchKernelGGL((k_trace_deep4<uint32_t>), dim3(db), dim3(kBlock), lds4, st, P);
+    return hipGetLastError();
+}
+
 hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
                         uint32_t blocks, hipStream_t st) {
     if (P.bvh_node && P.scene_kind == SCN_TRI) {
@@ -2514,18 +2531,7 @@ hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* 
             else
                 hipLaunchKernelGGL((k_trace_2a<kMaxLights>), dim3(blocks), dim3(kBlock), lds_a, st, P, list, count, zero);
             if (e == hipSuccess) e = hipGetLastError();
-            if (e != hipSuccess) return e;
-            // persistent: up to 2048 blocks (8 per CU), each serving partition blockIdx % n_part
-            if (!P.bvh4 || P.bvh4_stack <= 0 || P.bvh4_stack > kBvh4Stack) return hipErrorInvalidValue;
-            const uint32_t db = P.n_part * std::max<uint32_t>(1u, std::min<uint32_t>(2048u / P.n_part,
-                                                                                    (P.deep_cap + kBlock - 1) / kBlock));
-            const bool small4 = P.bvh4_nodes <= 0x10000;
-            const size_t ntop4 = std::min<size_t>((size_t)P.bvh4_nodes, kBvhTopNodes);
-            const size_t lds4 = ntop4 * 8 * sizeof(f4) +
-                                (size_t)P.bvh4_stack * kBlock * (small4 ? sizeof(uint16_t) : sizeof(uint32_t));
-            if (small4) hipLaunchKernelGGL((k_trace_deep4<uint16_t>), dim3(db), dim3(kBlock), lds4, st, P);
-            else hipLaunchKernelGGL((k_trace_deep4<uint32_t>), dim3(db), dim3(kBlock), lds4, st, P);
-            return hipGetLastError();
+            return e;   // phase B: launch_trace_deep
         }
         if (small && nl1)
             hipLaunchKernelGGL((k_trace_bvh<1, uint16_t>), dim3(blocks), dim3(kBlock), lds, st, P, list, count, zero);
@@ -2721,6 +2727,7 @@ hipError_t launch_query(const KParams& P, const float* rays, const float* tmax, 
     KParams Q = P;
     Q.sstep = nullptr;
     if (e == hipSuccess) e = launch_trace(Q, list, count, zero, blocks, st);
+    if (e == hipSuccess) e = launch_trace_deep(Q, st);
     if (e != hipSuccess) return e;
     switch (P.scene_kind) {
         case SCN_TRI: hipLaunchKernelGGL(k_query_out<SCN_TRI>, dim3(blocks), dim3(kBlock), 0, st, P, mode, out); break;

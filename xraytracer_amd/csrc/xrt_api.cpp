@@ -2,6 +2,7 @@
 // wavefront pass schedule that replaces NormalRenderer::render / ParallelRenderer::render
 // (Src/renderer.cpp:8-27, 83-99).
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <chrono>
@@ -12,6 +13,7 @@
 #include <unordered_map>
 #include <cfloat>
 #include <string>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -65,7 +67,6 @@ struct xrt_ctx {
     DevBuf q_rays, q_tmax, q_out;
     DevBuf brick_table, brick_data;   // sparse medium (xrt_set_medium_bricks)
     DevBuf stage;              // multi: device-output staging on subs[0] (accumulate from a device image)
-    std::unordered_map<uint32_t, bool> cdiv_cache;   // cdiv_exact results by divisor bits
 };
 
 namespace {
@@ -138,32 +139,46 @@ int setup_deep(xrt_ctx* c, KParams& P) {
 // enough to be subnormal is far below ulp(q) / 2 and cannot change the result), so one
 // binade decides it: all 2^23 mantissas of x in [1, 2) are compared with the host's IEEE
 // division (SSE, correctly rounded).  c is limited to [2^-4, 2^20] so the window's quotients
-// stay normal.  About 10 ms per divisor on 8 threads; results are cached per context.
-bool cdiv_exact(xrt_ctx* c, float d) {
+// stay normal.  About 10 ms per divisor on 8 threads.  Results are cached process-wide
+// (all contexts, including the sub-contexts of xrt_create_multi, share one table under a
+// mutex, so a multi-GPU render proves each divisor once), and the check uses at most as many
+// threads as the process's CPU affinity mask allows (capped at 8).
+bool cdiv_exact(xrt_ctx*, float d) {
     if (!(d >= 0x1p-4f && d <= 0x1p20f)) return false;
     uint32_t key;
     std::memcpy(&key, &d, 4);
-    auto it = c->cdiv_cache.find(key);
-    if (it != c->cdiv_cache.end()) return it->second;
+    static std::mutex mu;
+    static std::unordered_map<uint32_t, bool> cache;
+    std::lock_guard<std::mutex> lock(mu);   // held during the check: concurrent callers wait for it
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
     const float rc = 1.0f / d;
-    constexpr int kThreads = 8;
-    bool part[kThreads];
+    int nthreads = 1;
+    {
+        cpu_set_t cs;
+        CPU_ZERO(&cs);
+        if (sched_getaffinity(0, sizeof(cs), &cs) == 0) nthreads = CPU_COUNT(&cs);
+        nthreads = std::max(1, std::min(nthreads, 8));
+    }
+    std::vector<char> part(nthreads, 1);
+    auto work = [&](int t) {
+        bool ok = true;
+        for (uint32_t m = (uint32_t)t; m < (1u << 23) && ok; m += (uint32_t)nthreads) {
+            const uint32_t xb = 0x3f800000u | m;
+            float x;
+            std::memcpy(&x, &xb, 4);
+            const float q = x * rc;
+            ok = std::fma(std::fma(-d, q, x), rc, q) == x / d;
+        }
+        part[t] = ok;
+    };
     std::vector<std::thread> th;
-    for (int t = 0; t < kThreads; ++t)
-        th.emplace_back([&, t] {
-            bool ok = true;
-            for (uint32_t m = (uint32_t)t; m < (1u << 23) && ok; m += kThreads) {
-                const uint32_t xb = 0x3f800000u | m;
-                float x;
-                std::memcpy(&x, &xb, 4);
-                const float q = x * rc;
-                ok = std::fma(std::fma(-d, q, x), rc, q) == x / d;
-            }
-            part[t] = ok;
-        });
+    for (int t = 1; t < nthreads; ++t) th.emplace_back(work, t);
+    work(0);
     bool ok = true;
-    for (int t = 0; t < kThreads; ++t) th[t].join(), ok &= part[t];
-    c->cdiv_cache[key] = ok;
+    for (auto& t : th) t.join();
+    for (char p : part) ok &= p != 0;
+    cache[key] = ok;
     return ok;
 }
 
@@ -903,6 +918,10 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
                 return launch_trace(P, lists[nxt], counts_at(nxt), counts_at(cur), blocks, c->stream);
             });
             if (e != hipSuccess) return hip_err(c, e, "k_trace");
+            if (P.two_level && P.bvh_node && P.scene_kind == SCN_TRI) {
+                e = launch(XRT_K_DEEP, [&] { return launch_trace_deep(P, c->stream); });
+                if (e != hipSuccess) return hip_err(c, e, "k_trace_deep4");
+            }
             // no k_refill: k_shade twists its slots' rings itself (wave_refill)
         }
         if (it % poll_every == poll_every - 1) {
@@ -952,6 +971,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
         std::fprintf(stderr, "\n");
     }
     S.segments = hs[0], S.shadow_rays = hs[1], S.draws = hs[2], S.rejected = hs[3], S.stalled = hs[4];
+    S.rng_twists = hs[7];
     S.schedule = !fused ? XRT_SCHED_WAVEFRONT
                  : merged ? XRT_SCHED_STEP_MERGED
                  : use_step_tri(P) ? XRT_SCHED_STEP_TRI : XRT_SCHED_STEP;
@@ -1128,6 +1148,7 @@ static int render_multi(xrt_ctx* m, const xrt_render_params* p, float* d_out, fl
             for (int k = 0; k < XRT_K_COUNT; ++k) T.kernel_ms[k] += S[i].kernel_ms[k], T.launches[k] += S[i].launches[k];
             T.samples += S[i].samples, T.segments += S[i].segments, T.shadow_rays += S[i].shadow_rays;
             T.draws += S[i].draws, T.rejected += S[i].rejected, T.stalled += S[i].stalled;
+            T.rng_twists += S[i].rng_twists;
             T.path_slots += S[i].path_slots;
             T.iterations = std::max(T.iterations, S[i].iterations);
         }

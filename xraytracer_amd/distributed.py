@@ -72,7 +72,11 @@ class ShardedRenderer:
     renderer: anything with HipRenderer.render_device's signature (one GPU per rank).
     render(scene, W, H, fb) renders this rank's rows into the device tensor `fb` (H, W, 3)
     float32 — zeros elsewhere — after the work already queued on torch's current stream,
-    then reduces the frame into rank `dst`.  Only rank `dst`'s `fb` holds the image."""
+    then reduces the frame into rank `dst`.  Only rank `dst`'s `fb` holds the image.
+
+    Only the overwrite mode is supported: with accumulate=True every rank's unowned rows would
+    keep their old contents and the SUM reduce would add them once per rank, so render()
+    raises ValueError for it."""
 
     def __init__(self, renderer, dist=None, dst: int = 0):
         self.renderer = renderer
@@ -88,6 +92,9 @@ class ShardedRenderer:
     def render(self, scene, width: int, height: int, fb, after_stream=None, **kw):
         if tuple(fb.shape) != (height, width, 3) or not fb.is_contiguous():
             raise ValueError(f"framebuffer must be a contiguous ({height}, {width}, 3) tensor, got {tuple(fb.shape)}")
+        if kw.get("accumulate"):
+            raise ValueError("ShardedRenderer supports only the overwrite mode (accumulate=False): a SUM reduce "
+                             "of row shards would add every rank's stale unowned rows")
         import torch
         if after_stream is None and fb.is_cuda:
             after_stream = torch.cuda.current_stream(fb.device).cuda_stream
