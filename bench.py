@@ -60,7 +60,7 @@ def cpu_quota():
 # y % shard_count == 0 of the workload's own image at `spp` samples per pixel.  The oracle
 # restates the reference's linear scans (no acceleration structure), so C3's 1,001 spheres
 # and C4's 51,236 triangles cost far more per sample than C2's 36 triangles.
-CPU_SAMPLE = {"C1": (1, 256), "C2": (1, 256), "C3": (16, 96), "C4": (256, 2), "C5": (1, 128)}
+CPU_SAMPLE = {"C1": (1, 256), "C2": (1, 256), "C3": (4, 96), "C4": (256, 2), "C5": (1, 512)}
 
 
 def cpu_baseline(cfg_name, cfg, spp=None):

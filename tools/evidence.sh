@@ -19,6 +19,10 @@ PY
 python3 "$R/tools/prof_summary.py" "$R/gpurun_out/$TAG" "$KPAT" --traffic "$CFG" "$R/profiles/traffic_$CFG.json" \
     --pmc "$CFG" "$R/profiles/pmc_$CFG.json" --csv "$R/gpurun_out/$TAG/pmc_dispatch.csv" > "$R/gpurun_out/$TAG/summary.txt"
 cp "$R/gpurun_out/$TAG/kt/kt_kernel_stats.csv" "$R/gpurun_out/$TAG/kt_kernel_stats.csv"
+# raw rocprofv3 output (every dispatch of every pass) can exceed gpurun's 64 MiB copy-back:
+# keep the summaries and the gzipped per-dispatch counters of the dominant kernel only
+gzip -f "$R/gpurun_out/$TAG/pmc_dispatch.csv"
+rm -rf "$R/gpurun_out/$TAG"/{kt,sq1,sq2,fetch,write}
 mkdir -p "$R/gpurun_out/profiles_new" && cp "$R/profiles/traffic_$CFG.json" "$R/profiles/pmc_$CFG.json" "$R/gpurun_out/profiles_new/"
 timeout -k 10 600 python3 "$R/bench.py" --config "$CFG" > "$R/gpurun_out/$TAG/bench.json"
 cat "$R/gpurun_out/$TAG/bench.json"
