@@ -149,7 +149,7 @@ typedef struct {
     uint32_t flags;          /* XRT_FLAG_*                                              */
     /* launch geometry of the merged schedule; 0 = chosen by the library from the shard's
      * slot count.  Results never depend on these (tests render every layout). */
-    uint32_t slots_per_wave;    /* 0, 4, 16, 32 or 64 path slots per 64-lane wave        */
+    uint32_t slots_per_wave;    /* 0, 4, 8, 16, 32 or 64 path slots per 64-lane wave     */
     uint32_t visits_per_launch; /* 0 or 1..128 path segments per slot per step launch    */
 } xrt_render_params;
 

@@ -346,25 +346,42 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const D
                           : G == 2 ? 0x5555555555555555ull
                                    : ~0ull)
                          << u;
+    // Candidates two at a time: both triangles' LDS loads are issued before either test, so
+    // a lane pays one LDS latency per pair of candidates (with few waves per SIMD — the tail of
+    // a shard — the loop is bound by that latency, not by issue).  An odd last candidate is
+    // tested twice (same key: harmless for the min and the or).
     unsigned long long bk = ~0ull;
-    for (uint64_t bits = group_or64<G>(tm[0]) & pat; bits; bits &= bits - 1ull) {
-        const uint32_t k = (uint32_t)__builtin_ctzll(bits);
-        float t;
-        if (ray_tri_nb(o, d, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t)) {
-            const unsigned long long key = ((unsigned long long)__float_as_uint(t) << 32) | k;
-            bk = key < bk ? key : bk;
-        }
+    for (uint64_t bits = group_or64<G>(tm[0]) & pat; bits;) {
+        const uint32_t k0 = (uint32_t)__builtin_ctzll(bits);
+        bits &= bits - 1ull;
+        const uint32_t k1 = bits ? (uint32_t)__builtin_ctzll(bits) : k0;
+        bits &= bits - 1ull;
+        const f4 a0 = L.tri[3 * k0], b0 = L.tri[3 * k0 + 1], c0 = L.tri[3 * k0 + 2];
+        const f4 a1 = L.tri[3 * k1], b1 = L.tri[3 * k1 + 1], c1 = L.tri[3 * k1 + 2];
+        float t0, t1;
+        const bool h0 = ray_tri_nb(o, d, xyz(a0), xyz(b0), xyz(c0), t0);
+        const bool h1 = ray_tri_nb(o, d, xyz(a1), xyz(b1), xyz(c1), t1);
+        const unsigned long long key0 = h0 ? ((unsigned long long)__float_as_uint(t0) << 32) | k0 : ~0ull;
+        const unsigned long long key1 = h1 ? ((unsigned long long)__float_as_uint(t1) << 32) | k1 : ~0ull;
+        const unsigned long long key = key0 < key1 ? key0 : key1;
+        bk = key < bk ? key : bk;
     }
     uint32_t oc = 0;
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
-        for (uint64_t bits = group_or64<G>(tm[1 + l]) & pat; bits; bits &= bits - 1ull) {
-            const uint32_t k = (uint32_t)__builtin_ctzll(bits);
-            float t;
-            if (ray_tri_nb(so[l], sd[l], xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t) &&
-                t < stm[l]) {
+        for (uint64_t bits = group_or64<G>(tm[1 + l]) & pat; bits;) {
+            const uint32_t k0 = (uint32_t)__builtin_ctzll(bits);
+            bits &= bits - 1ull;
+            const uint32_t k1 = bits ? (uint32_t)__builtin_ctzll(bits) : k0;
+            bits &= bits - 1ull;
+            const f4 a0 = L.tri[3 * k0], b0 = L.tri[3 * k0 + 1], c0 = L.tri[3 * k0 + 2];
+            const f4 a1 = L.tri[3 * k1], b1 = L.tri[3 * k1 + 1], c1 = L.tri[3 * k1 + 2];
+            float t0, t1;
+            const bool h0 = ray_tri_nb(so[l], sd[l], xyz(a0), xyz(b0), xyz(c0), t0) && t0 < stm[l];
+            const bool h1 = ray_tri_nb(so[l], sd[l], xyz(a1), xyz(b1), xyz(c1), t1) && t1 < stm[l];
+            if (h0 || h1) {
                 oc |= 1u << l;
-                bits = 1ull;   // occluded: the loop update clears the rest
+                bits = 0ull;   // occluded: the rest need no test
             }
         }
     }
@@ -601,10 +618,19 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
             if (k >= spp) st = ST_DONE;
         };
         // jitter draws + PinholeCamera::sampleRay for the next sample (Src/renderer.cpp:44-50)
+#ifdef XRT_EXP_CHEAPSTART   // cost-map experiment builds only: the pixel-centre ray, NOT exact
+        v3 o_c, d_c;
+        camera_ray(P, div_w(P, (float)(int)col + 0.5f), div_h(P, (float)(int)row + 0.5f), o_c, d_c);
+#endif
         auto start_sample = [&]() {
+#ifdef XRT_EXP_CHEAPSTART
+            (void)rng.next(), (void)rng.next();
+            o = o_c, d = d_c;
+#else
             const float u = div_w(P, (float)(int)col + rng.next());
             const float v = div_h(P, (float)(int)row + rng.next());
             camera_ray(P, u, v, o, d);
+#endif
             thr = mk(1, 1, 1), rad = mk(0, 0, 0);
             depth = 0;
             ext = true;
@@ -940,6 +966,7 @@ static void launch_merged_i(const KParams& P, const KParams* dP, const StepObjs&
 uint32_t step_merged_spw(const KParams& P, uint64_t live) {
     const bool group = P.n_tris <= 64 && !(P.rflags & XRT_FLAG_NO_GROUP);   // 4 slots per wave: group traces only
     if (P.spw_req == 4) return group ? 4u : 16u;
+    if (P.spw_req == 8) return group ? 8u : 16u;
     if (P.spw_req == 16 || P.spw_req == 32 || P.spw_req == 64) return P.spw_req;
     // measured on C2 (tools/shard_sim.py): full waves down to ~160k live
     // slots, 32 slots per wave down to ~90k, 16 (4 lanes per slot) down to kMergedLive16,
@@ -968,6 +995,7 @@ static void launch_merged_spw(const KParams& P, const KParams* dP, const StepObj
         case 64: if (lane64) XRT_MERGED_CASE(64, 1, true); else XRT_MERGED_CASE(64, 1, false); break;
         case 32: if (group) XRT_MERGED_CASE(32, 2, true); else XRT_MERGED_CASE(32, 1, false); break;
         case 4: XRT_MERGED_CASE(4, 16, true); break;   // only with group traces (step_merged_spw)
+        case 8: XRT_MERGED_CASE(8, 8, true); break;    // only with group traces (step_merged_spw)
         default: if (group) XRT_MERGED_CASE(16, 4, true); else XRT_MERGED_CASE(16, 1, false); break;
     }
 #undef XRT_MERGED_CASE

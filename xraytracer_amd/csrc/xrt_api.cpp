@@ -696,9 +696,9 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
         return set_err(c, XRT_ERR_STATE, "VolumePathTracing needs xrt_set_medium first");
     if (p->integrator == XRT_INTEGRATOR_VPT_NEE && c->base.n_lights == 0)
         return set_err(c, XRT_ERR_STATE, "VolumePathTracingNEE needs an area light");
-    if (p->slots_per_wave != 0 && p->slots_per_wave != 4 && p->slots_per_wave != 16 && p->slots_per_wave != 32 &&
-        p->slots_per_wave != 64)
-        return set_err(c, XRT_ERR_INVALID, "slots_per_wave must be 0, 4, 16, 32 or 64");
+    if (p->slots_per_wave != 0 && p->slots_per_wave != 4 && p->slots_per_wave != 8 && p->slots_per_wave != 16 &&
+        p->slots_per_wave != 32 && p->slots_per_wave != 64)
+        return set_err(c, XRT_ERR_INVALID, "slots_per_wave must be 0, 4, 8, 16, 32 or 64");
     if (p->visits_per_launch > 128) return set_err(c, XRT_ERR_INVALID, "visits_per_launch must be 0..128");
     HIPCHK(c, hipSetDevice(c->device));
     if (wait == 1) {
