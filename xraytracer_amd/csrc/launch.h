@@ -48,7 +48,8 @@ size_t step_merged_lds_bytes(const KParams& P);
 void build_step_objs(const DObjBox* boxes, const DObjPlane* planes, int n, StepObjs& SO);
 hipError_t launch_step_merged(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                               const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
-                              uint32_t* req_count, uint32_t visits, uint64_t live, hipStream_t st);
+                              uint32_t* req_count, uint32_t visits, uint64_t live, uint32_t live_part_max,
+                              hipStream_t st);
 // the merged schedule's refill (leaves ST_RNGREQ to the merged kernel; see step_tri.hip)
 hipError_t launch_refill_merged(const KParams& P, const uint32_t* count, uint32_t* zero_count, hipStream_t st);
 hipError_t launch_finish(const KParams& P, hipStream_t st);

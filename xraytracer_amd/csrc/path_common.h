@@ -236,6 +236,39 @@ __device__ __forceinline__ void wave_refill(const KParams& P, bool want, uint32_
     }
 }
 
+// Cross-lane reductions within groups of G = 2, 4, 8 or 16 adjacent lanes by DPP (no LDS):
+// quad_perm swaps for 2 and 4, row_half_mirror / row_mirror for 8 and 16.  Every lane of
+// a group must be active.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, false);
+}
+template <int G>
+__device__ __forceinline__ uint32_t group_or32(uint32_t x) {
+    if (G >= 2) x |= dpp32<0xB1>(x);    // quad_perm(1, 0, 3, 2): partner lane ^ 1
+    if (G >= 4) x |= dpp32<0x4E>(x);    // quad_perm(2, 3, 0, 1): partner lane ^ 2
+    if (G >= 8) x |= dpp32<0x141>(x);   // row_half_mirror: lane 7 - i of its 8 (quads 0 and 1)
+    if (G >= 16) x |= dpp32<0x140>(x);  // row_mirror: lane 15 - i of its 16 (halves 0 and 1)
+    return x;
+}
+template <int G>
+__device__ __forceinline__ uint64_t group_or64(uint64_t x) {
+    return ((uint64_t)group_or32<G>((uint32_t)(x >> 32)) << 32) | group_or32<G>((uint32_t)x);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t min64_dpp(uint64_t x) {
+    const uint64_t y = ((uint64_t)dpp32<CTRL>((uint32_t)(x >> 32)) << 32) | dpp32<CTRL>((uint32_t)x);
+    return y < x ? y : x;
+}
+template <int G>
+__device__ __forceinline__ uint64_t group_min64(uint64_t x) {
+    if (G >= 2) x = min64_dpp<0xB1>(x);
+    if (G >= 4) x = min64_dpp<0x4E>(x);
+    if (G >= 8) x = min64_dpp<0x141>(x);
+    if (G >= 16) x = min64_dpp<0x140>(x);
+    return x;
+}
+
 // Append v to list (count at cnt) for every lane with want set: one atomic per wave.
 // Must be called by every lane of the wave (wave-uniform control flow).
 __device__ __forceinline__ void wave_append(bool want, uint32_t v, uint32_t* list, uint32_t* cnt, int lane) {

@@ -281,36 +281,6 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
 // the group by DPP, lane u tests the candidate triangles k = u (mod G) in increasing k, and
 // the group reduces by DPP: min of (t bits << 32 | k) for the extension ray — smallest t,
 // then lowest index, the reference's in-order `t < best` scan — and OR of occlusion bits.
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, false);
-}
-template <int G>
-__device__ __forceinline__ uint32_t group_or32(uint32_t x) {
-    if (G >= 2) x |= dpp32<0xB1>(x);    // quad_perm(1, 0, 3, 2): partner lane ^ 1
-    if (G >= 4) x |= dpp32<0x4E>(x);    // quad_perm(2, 3, 0, 1): partner lane ^ 2
-    if (G >= 8) x |= dpp32<0x141>(x);   // row_half_mirror: lane 7 - i of its 8 (quads 0 and 1)
-    if (G >= 16) x |= dpp32<0x140>(x);  // row_mirror: lane 15 - i of its 16 (halves 0 and 1)
-    return x;
-}
-template <int G>
-__device__ __forceinline__ uint64_t group_or64(uint64_t x) {
-    return ((uint64_t)group_or32<G>((uint32_t)(x >> 32)) << 32) | group_or32<G>((uint32_t)x);
-}
-template <int CTRL>
-__device__ __forceinline__ uint64_t min64_dpp(uint64_t x) {
-    const uint64_t y = ((uint64_t)dpp32<CTRL>((uint32_t)(x >> 32)) << 32) | dpp32<CTRL>((uint32_t)x);
-    return y < x ? y : x;
-}
-template <int G>
-__device__ __forceinline__ uint64_t group_min64(uint64_t x) {
-    if (G >= 2) x = min64_dpp<0xB1>(x);
-    if (G >= 4) x = min64_dpp<0x4E>(x);
-    if (G >= 8) x = min64_dpp<0x141>(x);
-    if (G >= 16) x = min64_dpp<0x140>(x);
-    return x;
-}
-
 template <int NL, int G>
 __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const DObjPlane* pl, int lane, bool ext, v3 o, v3 d,
                                             uint32_t shm, const v3 (&so)[NL + 1], const v3 (&sd)[NL + 1],
@@ -945,9 +915,11 @@ void build_step_objs(const DObjBox* boxes, const DObjPlane* planes, int n, StepO
 template <int INTEG, int SPW, int G, bool LANE>
 static void launch_merged_i(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                             const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
-                            uint32_t* req_count, uint32_t visits, size_t lds, hipStream_t st) {
+                            uint32_t* req_count, uint32_t visits, uint32_t part_live, size_t lds, hipStream_t st) {
+    // one block per per_block live entries of the fullest partition (part_iter strides over
+    // any remainder, so an upper bound on the live count is all the grid needs)
     const uint32_t per_block = (kBlock / 64) * SPW;
-    const uint32_t blocks = P.n_part * ((P.part_cap + per_block - 1) / per_block);
+    const uint32_t blocks = P.n_part * ((std::min(part_live, P.part_cap) + per_block - 1) / per_block);
 #define XRT_LAUNCH_MERGED(NLV)                                                                                       \
     hipLaunchKernelGGL((k_step_merged<INTEG, NLV, SPW, G, LANE>), dim3(blocks), dim3(kBlock), lds, st, dP, SO, list, count, \
                        out, out_count, zero, req_count, visits)
@@ -986,11 +958,12 @@ uint32_t step_merged_group(const KParams& P, uint32_t spw) {
 template <int INTEG>
 static void launch_merged_spw(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                               const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
-                              uint32_t* req_count, uint32_t visits, uint64_t live, size_t lds, hipStream_t st) {
+                              uint32_t* req_count, uint32_t visits, uint64_t live, uint32_t part_live, size_t lds,
+                              hipStream_t st) {
     const bool group = P.n_tris <= 64 && !(P.rflags & XRT_FLAG_NO_GROUP);   // group trace: 64-bit triangle masks
     const bool lane64 = group && exp_env("XRT_LANE_TRACE");   // experiment: per-lane traces, full waves
 #define XRT_MERGED_CASE(SPWV, GV, LV) \
-    launch_merged_i<INTEG, SPWV, GV, LV>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, lds, st)
+    launch_merged_i<INTEG, SPWV, GV, LV>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, part_live, lds, st)
     switch (step_merged_spw(P, live)) {
         case 64: if (lane64) XRT_MERGED_CASE(64, 1, true); else XRT_MERGED_CASE(64, 1, false); break;
         case 32: if (group) XRT_MERGED_CASE(32, 2, true); else XRT_MERGED_CASE(32, 1, false); break;
@@ -1003,14 +976,15 @@ static void launch_merged_spw(const KParams& P, const KParams* dP, const StepObj
 
 hipError_t launch_step_merged(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                               const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
-                              uint32_t* req_count, uint32_t visits, uint64_t live, hipStream_t st) {
+                              uint32_t* req_count, uint32_t visits, uint64_t live, uint32_t live_part_max,
+                              hipStream_t st) {
     const size_t lds = step_merged_lds_bytes(P);
     if (P.integrator == XRT_INTEGRATOR_DIRECT)
         launch_merged_spw<XRT_INTEGRATOR_DIRECT>(P, dP, SO, list, count, out, out_count, zero, req_count, visits,
-                                                 live, lds, st);
+                                                 live, live_part_max, lds, st);
     else
         launch_merged_spw<XRT_INTEGRATOR_GI>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, live,
-                                             lds, st);
+                                             live_part_max, lds, st);
     return hipGetLastError();
 }
 

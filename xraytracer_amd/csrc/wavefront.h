@@ -120,6 +120,7 @@ struct StepObjs {
 constexpr uint32_t kBvhLeaf = 4;      // BVH: primitives per leaf (at most)
 constexpr int kBvhMaxDepth = 48;      // BVH build: depth bound (SAH above max - 24 levels, median below)
 constexpr int kBvhStack = 24;         // k_trace_bvh: LDS traversal stack entries per thread (> tree depth)
+constexpr uint32_t kDeepQuadSlots = 0xffffffffu;   // path slots below which k_trace_deep4q runs (tuned: DESIGN.md §3)
 constexpr int kBvh4Stack = 48;        // k_trace_deep4: LDS stack entries per lane (>= 3 * 4-wide depth + 1)
 constexpr int kSphBvhMin = 16;        // sphere scenes with at least this many spheres get a skip-link BVH
 constexpr int kSmallTris = 1024;   // scenes up to this size keep every triangle in LDS
@@ -183,6 +184,7 @@ struct KParams {
                                     // merged-trace records when n_sobj <= kMergedMaxObjs, else null
     const f4* bvh4;           // the BVH's 4-wide form (bvh.h Bvh4Node, 8 f4 each) for k_trace_deep4
     int bvh4_nodes, bvh4_stack;   // node count; LDS stack entries per lane (3 * depth + 1)
+    int deep_quad;                // k_trace_deep4q (four lanes per ray) instead of k_trace_deep4
     uint32_t* deep;           // queued rays (slot * 8 + kind: 0 extension, 1 + l shadow ray l), per partition
     uint32_t* deep_count;     // [kMaxParts] counts, then [kMaxParts] fetch counters
     uint32_t deep_cap;        // entries per partition

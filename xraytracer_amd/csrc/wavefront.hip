@@ -602,6 +602,122 @@ __global__ __launch_bounds__(kBlock, XRT_DEEP_WAVES) void k_trace_deep4(KParams 
 #endif
 }
 
+// Phase B with four lanes per ray ("quad"): lane q of a quad owns child q of the current
+// node — loads its two float4, tests its box and, for a leaf child, that leaf's triangles —
+// and the quad combines by DPP quad_perm: the closest hit as the minimum of (t bits, index
+// + 1) (the lexicographic (t, index) order of bvh_leaf's update; a lane that found nothing
+// better still holds the ray's current hit), occlusion as an or, the next node as the
+// nearest overlapping interior child (ties to the lower child) with the other overlapping
+// ones pushed.  A step costs one node fetch and at most one leaf's tests per lane instead of
+// four boxes and up to four leaves, so the longest walk of a launch — which bounds the
+// launch when few rays are queued (a row shard of a multi-GPU frame) — takes fewer cycles.
+// Exact for the same reason as k_trace_deep4: every triangle whose padded box overlaps
+// [0, best t] is tested, whatever the order.  Rays are fetched a quad at a time with the
+// same partitioned queue and counters.
+template <typename SE>
+__global__ __launch_bounds__(kBlock, XRT_DEEP_WAVES) void k_trace_deep4q(KParams P) {
+    extern __shared__ uint32_t bvh_stack_lds[];
+    constexpr int kQuads = kBlock / 4;
+    const int tid = threadIdx.x, lane = tid & 63, q = lane & 3;
+    const int ntop = P.bvh4_nodes < (int)kBvhTopNodes ? P.bvh4_nodes : (int)kBvhTopNodes;
+    f4* top = reinterpret_cast<f4*>(bvh_stack_lds);
+    for (int i = tid; i < 8 * ntop; i += kBlock) top[i] = P.bvh4[i];
+    SE* stk = reinterpret_cast<SE*>(bvh_stack_lds + 32 * ntop) + (tid >> 2);   // one stack per quad
+    __syncthreads();
+    const uint32_t p = blockIdx.x % P.n_part;
+    const uint32_t cnt = P.deep_count[p];
+    uint32_t* next_ctr = P.deep_count + kMaxParts + p;
+    const uint32_t* dq = P.deep + (size_t)p * P.deep_cap;
+    constexpr uint64_t kLeads = 0x1111111111111111ull;   // lane 0 of every quad
+    bool active = false, drained = cnt == 0, any = false;
+    uint32_t s = 0, l = 0;
+    int node = 0, sp = 0, bk = -1;
+    v3 o = mk(0, 0, 0), d = mk(0, 0, 0), inv = mk(0, 0, 0);
+    float tmax = 0.0f, bt = kINF, bu = 0.0f, bv = 0.0f;
+    while (true) {
+        const uint64_t idle = __ballot(!active) & kLeads;
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        if (!drained && (nidle >= 4u || nidle == 16u)) {
+            const int leader = __ffsll((unsigned long long)idle) - 1;
+            uint32_t b = 0;
+            if (lane == leader) b = atomicAdd(next_ctr, nidle);
+            b = (uint32_t)__builtin_amdgcn_readlane((int)b, leader);
+            if (b + nidle >= cnt) drained = true;
+            if (!active) {
+                const uint32_t idx = b + (uint32_t)__popcll(idle & ((1ull << (lane & ~3)) - 1ull));
+                if (idx < cnt) {
+                    const uint32_t e = dq[idx];
+                    s = e >> 3;
+                    const uint32_t kind = e & 7u;
+                    any = kind != 0;
+                    if (!any) {
+                        o = xyz(P.ray_o[s]), d = xyz(P.ray_d[s]);
+                        const f4 h = P.hit[s];
+                        bt = h.x, bu = h.y, bv = h.z, bk = __float_as_int(h.w);
+                        tmax = kINF;
+                    } else {
+                        l = kind - 1u;
+                        const f4 a = P.sh_o[(size_t)l * P.n_slots + s];
+                        o = xyz(a), tmax = a.w;
+                        d = xyz(P.sh_d[(size_t)l * P.n_slots + s]);
+                        bt = kINF, bk = -1;
+                    }
+                    inv = rcp3(d);
+                    node = 0, sp = 0;
+                    active = true;
+                }
+            }
+        }
+        if (!__ballot(active)) break;
+        if (!active) continue;
+        // ---- one node: child q on lane q
+        const f4* N = node < ntop ? top + 8 * node : P.bvh4 + 8 * (size_t)node;
+        const f4 lo = N[q], hi = N[4 + q];
+        const int cidx = __float_as_int(lo.w), ccnt = __float_as_int(hi.w);
+        const float e = ccnt >= 0 ? bvh_enter(lo, hi, o, inv, any ? tmax : bt) : __builtin_inff();
+        bool done;
+        if (any) {
+            bool occ = false;
+            if (ccnt > 0 && e != __builtin_inff()) occ = bvh_leaf_batch<true>(P, cidx, ccnt, o, d, tmax, bt, bu, bv, bk);
+            done = group_or32<4>(occ ? 1u : 0u) != 0u;
+            if (done && q == 0) atomicOr(P.occ + s, 1u << l);
+        } else {
+            float t1 = bt, u1 = bu, v1 = bv;
+            int k1 = bk;
+            if (ccnt > 0 && e != __builtin_inff()) (void)bvh_leaf_batch<false>(P, cidx, ccnt, o, d, kINF, t1, u1, v1, k1);
+            const uint64_t key = ((uint64_t)__float_as_uint(t1) << 32) | (uint32_t)(k1 + 1);
+            const uint64_t kmin = group_min64<4>(key);
+            const bool win = key == kmin;   // lanes holding the minimum hold the same (u, v)
+            bu = __uint_as_float(group_or32<4>(win ? __float_as_uint(u1) : 0u));
+            bv = __uint_as_float(group_or32<4>(win ? __float_as_uint(v1) : 0u));
+            bt = __uint_as_float((uint32_t)(kmin >> 32));
+            bk = (int)(uint32_t)kmin - 1;
+            done = false;
+        }
+        if (!done) {
+            const float lim = any ? tmax : bt;
+            const bool inner = ccnt == 0 && e <= lim;   // interior child still overlapping [0, lim]
+            const uint64_t nkey = inner ? (((uint64_t)__float_as_uint(e) << 32) | (uint32_t)q) : ~0ull;
+            const uint64_t nmin = group_min64<4>(nkey);
+            if (nmin != ~0ull) {
+                const bool nearest = nkey == nmin;
+                const uint32_t m4 = (uint32_t)(__ballot(inner && !nearest) >> (lane & ~3)) & 0xfu;
+                if (inner && !nearest) stk[(sp + __popc(m4 & ((1u << q) - 1u))) * kQuads] = (SE)cidx;
+                sp += __popc(m4);
+                node = (int)group_or32<4>(nearest ? (uint32_t)cidx : 0u);
+            } else if (sp == 0) {
+                done = true;
+            } else {
+                node = (int)stk[(--sp) * kQuads];
+            }
+        }
+        if (done) {
+            if (!any && q == 0) P.hit[s] = make_float4(bt, bu, bv, __int_as_float(bk));
+            active = false;
+        }
+    }
+}
+
 // Small triangle scenes (<= kSmallTris triangles, e.g. the Cornell box): every triangle
 // and the per-object boxes live in LDS for the whole launch; objects are visited in
 // Scene iteration order and a wave skips an object none of its rays can hit (closest-hit
@@ -2505,6 +2621,13 @@ hipError_t launch_trace_deep(const KParams& P, hipStream_t st) {
     const bool small4 = P.bvh4_nodes <= 0x10000;
     const size_t ntop4 = std::min<size_t>((size_t)P.bvh4_nodes, kBvhTopNodes);
     const size_t lds4 = ntop4 * 8 * sizeof(f4) + (size_t)P.bvh4_stack * kBlock * (small4 ? sizeof(uint16_t) : sizeof(uint32_t));
+    if (P.deep_quad) {   // four lanes per ray: one stack per quad
+        const size_t lds4q = ntop4 * 8 * sizeof(f4) +
+                             (size_t)P.bvh4_stack * (kBlock / 4) * (small4 ? sizeof(uint16_t) : sizeof(uint32_t));
+        if (small4) hipLaunchKernelGGL((k_trace_deep4q<uint16_t>), dim3(db), dim3(kBlock), lds4q, st, P);
+        else hipLaunchKernelGGL((k_trace_deep4q<uint32_t>), dim3(db), dim3(kBlock), lds4q, st, P);
+        return hipGetLastError();
+    }
     if (small4) hipLaunchKernelGGL((k_trace_deep4<uint16_t>), dim3(db), dim3(kBlock), lds4, st, P);
     else hipLaunchKernelGGL((k_trace_deep4<uint32_t>), dim3(db), dim3(kBlock), lds4, st, P);
     return hipGetLastError();

@@ -433,7 +433,7 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
     // hit position, so box tests never drop a hit the linear scan accepts.
     P.bvh_node = nullptr, P.bvh_tri = nullptr, P.bvh_stack = 0, P.bvh_nodes = 0;
     P.stri = nullptr, P.sbox = nullptr, P.splane = nullptr, P.n_stri = 0, P.n_sobj = 0, P.two_level = 0;
-    P.sstep = nullptr, P.bvh4 = nullptr, P.bvh4_nodes = 0, P.bvh4_stack = 0;
+    P.sstep = nullptr, P.bvh4 = nullptr, P.bvh4_nodes = 0, P.bvh4_stack = 0, P.deep_quad = 0;
     if (P.scene_kind == SCN_TRI && !P.small_tri && P.n_tris > 0 && !exp_env("XRT_NO_BVH")) {
         // two-level split: mesh objects of more than kLargeObjTris triangles go into the BVH,
         // the rest (if any, and if they fit the LDS scan) are scanned directly
@@ -758,6 +758,12 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     P.cdiv = (cdiv_exact(c, P.fw) ? 1u : 0u) | (cdiv_exact(c, P.fh) ? 2u : 0u) | (cdiv_exact(c, P.aspect) ? 4u : 0u);
     P.shard_index = p->shard_index, P.shard_count = p->shard_count, P.n_slots = (uint32_t)n;
     P.spw_req = p->slots_per_wave, P.rflags = p->flags;
+    // two-level traces: four lanes per queued ray below kDeepQuadSlots path slots (the deep
+    // walk's launch is then bound by its longest walk, not by its total work)
+    {
+        const char* dq = exp_env("XRT_DEEP_QUAD");
+        P.deep_quad = dq ? std::atoi(dq) : (n < kDeepQuadSlots ? 1 : 0);
+    }
     // live-list partitions: up to kMaxParts (a multiple of the 8 XCDs), >= 2048 slots each
     {
         uint32_t np = (uint32_t)std::min<size_t>(kMaxParts, std::max<size_t>(1, n / 2048));
@@ -878,12 +884,19 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     if ((rc = ensure(c, c->kparams, sizeof(KParams)))) return rc;
     HIPCHK(c, hipMemcpyAsync(c->kparams.p, &P, sizeof(KParams), hipMemcpyHostToDevice, c->stream));
     const KParams* dP = as<KParams>(c->kparams);
-    const uint64_t poll_every = merged ? 2 : fused ? 4 : kPoll, ahead = merged ? 6 : fused ? 16 : kAhead;
+    // the merged schedule polls every launch and runs at most 3 launches ahead of the last
+    // retired poll, so its per-launch layout (below) follows the live count closely
+    const uint64_t poll_every = merged ? 1 : fused ? 4 : kPoll, ahead = merged ? 3 : fused ? 16 : kAhead;
     // merged schedule: the slots-per-wave layout is chosen from the shard's slot count (full
     // waves for a whole frame, 2 or 4 lanes per slot for small pixel shards); switching it
     // as the live count drops measured slower.  Every layout gives identical
     // results.
-    const uint64_t live_hint = n;
+    // The merged schedule re-chooses the layout every launch from the live count of the last
+    // retired poll (an upper bound: paths only finish), so a frame's tail, where few slots
+    // remain, runs with more lanes per slot, and sizes the grid by the fullest
+    // partition's live count instead of its capacity.  Results never depend on the layout.
+    uint64_t live_hint = n;
+    uint32_t live_part_max = P.part_cap;
     std::vector<uint64_t> launch_live;   // the live hint each step launch was sized with
     size_t step_idx = 0;
     for (; it < cap_iters && !done; ++it) {
@@ -897,7 +910,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
                 if (merged)
                     return launch_step_merged(P, dP, c->step_objs, lists[cur], counts_at(ci), lists[nxt],
                                               counts_at(co), counts_at(cz), req_counts + (epoch & 1) * kMaxParts,
-                                              step_visits, live_hint, c->stream);
+                                              step_visits, live_hint, live_part_max, c->stream);
                 return launch_step(P, dP, lists[cur], counts_at(ci), lists[nxt], counts_at(co), counts_at(cz),
                                    req_counts + (epoch & 1) * kMaxParts, step_visits, blocks, c->stream);
             });
@@ -938,8 +951,11 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             if (!must_wait && hipEventQuery(q.ev) != hipSuccess) break;
             HIPCHK(c, hipEventSynchronize(q.ev));
             uint64_t alive = 0;
-            for (uint32_t k = 0; k < P.n_part; ++k) alive += c->h_poll[q.slot * kMaxParts + k];
+            uint32_t pmax = 0;
+            for (uint32_t k = 0; k < P.n_part; ++k)
+                alive += c->h_poll[q.slot * kMaxParts + k], pmax = std::max(pmax, c->h_poll[q.slot * kMaxParts + k]);
             if (alive == 0) done = true;
+            if (merged && !P.spw_req && alive < live_hint) live_hint = alive, live_part_max = std::max(1u, pmax);
             polls.erase(polls.begin());
             if (done) break;
         }
@@ -978,7 +994,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     S.partitions = P.n_part;
     if (fused) S.visits_per_launch = step_visits;
     if (merged) {
-        S.slots_per_wave = step_merged_spw(P, live_hint);
+        S.slots_per_wave = step_merged_spw(P, n);   // the layout of the first launch
         S.group_lanes = step_merged_group(P, S.slots_per_wave);
     }
     if (timing) {
