@@ -125,16 +125,20 @@ def test_c3_geometry(renderer):
     counters_equal(g, st)
 
 
-def test_c4_mesh_geometry(renderer):
+@pytest.mark.parametrize("deep", ["auto", "single", "quad"])
+def test_c4_mesh_geometry(renderer, deep):
     """C4's own mesh: SphereMesh(nTheta = nPhi = 160) = 51,200 triangles + the Cornell box
-    (51,236), at C4's 16:9 aspect (160x90): wavefront schedule with the BVH trace."""
+    (51,236), at C4's 16:9 aspect (160x90): wavefront schedule with the two-level trace, the
+    BVH walked with four lanes per queued ray (what row shards run) and with one (what the
+    full 1920x1080 frame runs, above 1.5M path slots)."""
     s = scenes.cornell_spheremesh(160, 90)
     assert s.desc.n_tris == 51200 + 36
     renderer.spp = 2
     renderer.upload(s)
-    img = renderer.render(s, 160, 90, timing=True)
+    img = renderer.render(s, 160, 90, timing=True, deep=deep)
     g = renderer.stats
     assert g.schedule == abi.XRT_SCHED_WAVEFRONT and g.launches[abi.XRT_K_STEP] == 0
+    assert g.launches[abi.XRT_K_DEEP] == g.launches[abi.XRT_K_TRACE] > 0
     ref, st = pyoracle.render(s, 160, 90, 2)
     compare(img, ref)
     counters_equal(g, st)

@@ -47,7 +47,7 @@ EXPECT_TRI = {"auto": abi.XRT_SCHED_STEP_MERGED, "step_tri": abi.XRT_SCHED_STEP_
               "wavefront": abi.XRT_SCHED_WAVEFRONT}
 
 
-GPU_ONLY = ("slots_per_wave", "visits_per_launch", "group")   # launch geometry, not semantics
+GPU_ONLY = ("slots_per_wave", "visits_per_launch", "group", "deep")   # launch geometry, not semantics
 
 
 def render_both(r, scene, w, h, spp, schedule="auto", **kw):
@@ -356,14 +356,15 @@ def test_normal_integrator_on_medium_box(renderer, sched):
     compare(img, ref)
 
 
+@pytest.mark.parametrize("deep", ["single", "quad"])
 @pytest.mark.parametrize("nt,w,h,spp", [(24, 64, 36, 4), (80, 48, 30, 3), (380, 12, 9, 2)])
-def test_c4_sphere_mesh_gi(renderer, nt, w, h, spp):
+def test_c4_sphere_mesh_gi(renderer, nt, w, h, spp, deep):
     """Config C4 scene family (Cornell + tessellated sphere; 1,152, 12,800 and 288,800 mesh
     triangles) at reduced size: the wavefront schedule with BVH traces, bit-exact against
     the oracle's linear scan, counters included.  The largest tree has more than 65,536
     nodes, so its traversal stack takes 32-bit entries (16-bit for the others)."""
     s = scenes.cornell_spheremesh(w, h, n_theta=nt, n_phi=nt)
-    img, ref, st = render_both(renderer, s, w, h, spp)
+    img, ref, st = render_both(renderer, s, w, h, spp, deep=deep)
     compare(img, ref)
     g = renderer.stats
     assert g.launches[abi.XRT_K_STEP] == 0   # too large for LDS: multi-pass schedule

@@ -762,7 +762,10 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     // walk's launch is then bound by its longest walk, not by its total work)
     {
         const char* dq = exp_env("XRT_DEEP_QUAD");
-        P.deep_quad = dq ? std::atoi(dq) : (n < kDeepQuadSlots ? 1 : 0);
+        P.deep_quad = dq                                  ? std::atoi(dq)
+                      : (p->flags & XRT_FLAG_DEEP_SINGLE) ? 0
+                      : (p->flags & XRT_FLAG_DEEP_QUAD)   ? 1
+                                                          : (n < kDeepQuadSlots ? 1 : 0);
     }
     // live-list partitions: up to kMaxParts (a multiple of the 8 XCDs), >= 2048 slots each
     {
@@ -955,7 +958,10 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             for (uint32_t k = 0; k < P.n_part; ++k)
                 alive += c->h_poll[q.slot * kMaxParts + k], pmax = std::max(pmax, c->h_poll[q.slot * kMaxParts + k]);
             if (alive == 0) done = true;
-            if (merged && !P.spw_req && alive < live_hint) live_hint = alive, live_part_max = std::max(1u, pmax);
+            if (alive < live_hint) {
+                live_hint = alive;
+                if (merged && !P.spw_req) live_part_max = std::max(1u, pmax);
+            }
             polls.erase(polls.begin());
             if (done) break;
         }

@@ -68,16 +68,20 @@ class HipRenderer:
 
     def params(self, scene, width, height, shard_index=0, shard_count=1, timing=False, integrator=None,
                max_depth=None, schedule="auto", slots_per_wave=0, visits_per_launch=0, group=True,
-               accumulate=False):
+               accumulate=False, deep="auto"):
         """schedule: "auto" (fused k_step when the scene fits in LDS — for small triangle
         scenes with merged shadow + extension traces — else the multi-pass wavefront),
         "wavefront" (always k_shade + k_trace) or "step_tri" (fused, one cooperative trace
         per ray kind instead of the merged traces).  slots_per_wave / visits_per_launch /
         group fix the merged schedule's launch geometry (0 / True = the library's choice);
         results never depend on them.  accumulate: add the samples to the output buffer's
-        current contents before the divide (XRT_FLAG_ACCUMULATE, Renderer::render's contract)."""
+        current contents before the divide (XRT_FLAG_ACCUMULATE, Renderer::render's contract).
+        deep: the two-level trace's BVH walk, "auto", "single" (one lane per queued ray) or
+        "quad" (four); results never depend on it."""
         if schedule not in ("auto", "wavefront", "step_tri"):
             raise ValueError(f"unknown schedule {schedule!r}")
+        if deep not in ("auto", "single", "quad"):
+            raise ValueError(f"unknown deep walk {deep!r}")
         p = abi.XrtRenderParams()
         p.integrator = abi.INTEGRATORS[integrator or scene.integrator]
         p.max_depth = scene.max_depth if max_depth is None else max_depth
@@ -85,7 +89,8 @@ class HipRenderer:
         p.shard_index, p.shard_count = shard_index, shard_count
         p.flags = ((abi.XRT_FLAG_TIMING if timing else 0) | (abi.XRT_FLAG_WAVEFRONT if schedule == "wavefront" else 0) |
                    (abi.XRT_FLAG_NO_MERGED if schedule == "step_tri" else 0) | (0 if group else abi.XRT_FLAG_NO_GROUP) |
-                   (abi.XRT_FLAG_ACCUMULATE if accumulate else 0))
+                   (abi.XRT_FLAG_ACCUMULATE if accumulate else 0) |
+                   {"auto": 0, "single": abi.XRT_FLAG_DEEP_SINGLE, "quad": abi.XRT_FLAG_DEEP_QUAD}[deep])
         p.slots_per_wave, p.visits_per_launch = slots_per_wave, visits_per_launch
         return p
 
