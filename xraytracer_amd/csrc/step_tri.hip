@@ -434,7 +434,8 @@ __global__ __launch_bounds__(kBlock, XRT_2A_WAVES) void k_trace_2a_coop(KParams 
         wave_append(valid && dext, s * 8u, dq, P.deep_count + it.p, lane);
 #pragma unroll
         for (int l = 0; l < NL; ++l)
-            wave_append(valid && ((dsh >> l) & 1u), s * 8u + 1u + (uint32_t)l, dq, P.deep_count + it.p, lane);
+            wave_append(valid && ((dsh >> l) & 1u), s * 8u + 1u + (uint32_t)l, dq + P.part_cap,
+                        P.deep_count + 2 * kMaxParts + it.p, lane);
         wave_sync();   // W is rewritten by the next round's rays
     }
 }

@@ -185,8 +185,10 @@ struct KParams {
     const f4* bvh4;           // the BVH's 4-wide form (bvh.h Bvh4Node, 8 f4 each) for k_trace_deep4
     int bvh4_nodes, bvh4_stack;   // node count; LDS stack entries per lane (3 * depth + 1)
     int deep_quad;                // k_trace_deep4q (four lanes per ray) instead of k_trace_deep4
-    uint32_t* deep;           // queued rays (slot * 8 + kind: 0 extension, 1 + l shadow ray l), per partition
-    uint32_t* deep_count;     // [kMaxParts] counts, then [kMaxParts] fetch counters
+    uint32_t* deep;           // queued rays (slot * 8 + kind: 0 extension, 1 + l shadow ray l), per partition:
+                              // extension rays from the start, shadow rays from entry part_cap on
+    uint32_t* deep_count;     // [kMaxParts] extension-ray counts, [kMaxParts] fetch counters,
+                              // [kMaxParts] shadow-ray counts (queued from dq + part_cap)
     uint32_t deep_cap;        // entries per partition
     const f4* snode;          // sphere scenes: threaded BVH (bvh.h SkipNode, 2 f4 each), else null
     const f4* ssph;           // spheres in BVH leaf order (center, radius)

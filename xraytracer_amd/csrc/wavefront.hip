@@ -442,7 +442,8 @@ __global__ __launch_bounds__(kBlock) void k_trace_2a(KParams P, const uint32_t* 
         wave_append(valid && dext, s * 8u, dq, P.deep_count + it.p, lane);
 #pragma unroll
         for (int l = 0; l < NL; ++l)
-            wave_append(valid && ((dsh >> l) & 1u), s * 8u + 1u + (uint32_t)l, dq, P.deep_count + it.p, lane);
+            wave_append(valid && ((dsh >> l) & 1u), s * 8u + 1u + (uint32_t)l, dq + P.part_cap,
+                        P.deep_count + 2 * kMaxParts + it.p, lane);
     }
 }
 
@@ -495,9 +496,13 @@ __global__ __launch_bounds__(kBlock, XRT_DEEP_WAVES) void k_trace_deep4(KParams 
     SE* stk = reinterpret_cast<SE*>(bvh_stack_lds + 32 * ntop) + tid;
     __syncthreads();
     const uint32_t p = blockIdx.x % P.n_part;
-    const uint32_t cnt = P.deep_count[p];
+    // extension rays first, then shadow rays (queued apart by phase A), so a wave's lanes
+    // mostly run the same kind of walk (closest hit or any hit) at a time
+    const uint32_t n_ext = P.deep_count[p];
+    const uint32_t cnt = n_ext + P.deep_count[2 * kMaxParts + p];
     uint32_t* next_ctr = P.deep_count + kMaxParts + p;
     const uint32_t* dq = P.deep + (size_t)p * P.deep_cap;
+    const uint32_t* dqs = dq + P.part_cap - n_ext;   // dqs[idx] for idx >= n_ext
 #ifdef XRT_EXPERIMENTS
     if (blockIdx.x < P.n_part && tid == 0) atomicAdd(P.stats + 38, (unsigned long long)cnt);
     uint32_t nsteps = 0, niter = 0;
@@ -523,7 +528,7 @@ __global__ __launch_bounds__(kBlock, XRT_DEEP_WAVES) void k_trace_deep4(KParams 
             if (!active) {
                 const uint32_t idx = b + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
                 if (idx < cnt) {
-                    const uint32_t e = dq[idx];
+                    const uint32_t e = idx < n_ext ? dq[idx] : dqs[idx];
                     s = e >> 3;
                     const uint32_t kind = e & 7u;
                     any = kind != 0;
@@ -625,9 +630,13 @@ __global__ __launch_bounds__(kBlock, XRT_DEEP_WAVES) void k_trace_deep4q(KParams
     SE* stk = reinterpret_cast<SE*>(bvh_stack_lds + 32 * ntop) + (tid >> 2);   // one stack per quad
     __syncthreads();
     const uint32_t p = blockIdx.x % P.n_part;
-    const uint32_t cnt = P.deep_count[p];
+    // extension rays first, then shadow rays (queued apart by phase A), so a wave's lanes
+    // mostly run the same kind of walk (closest hit or any hit) at a time
+    const uint32_t n_ext = P.deep_count[p];
+    const uint32_t cnt = n_ext + P.deep_count[2 * kMaxParts + p];
     uint32_t* next_ctr = P.deep_count + kMaxParts + p;
     const uint32_t* dq = P.deep + (size_t)p * P.deep_cap;
+    const uint32_t* dqs = dq + P.part_cap - n_ext;   // dqs[idx] for idx >= n_ext
     constexpr uint64_t kLeads = 0x1111111111111111ull;   // lane 0 of every quad
     bool active = false, drained = cnt == 0, any = false;
     uint32_t s = 0, l = 0;
@@ -646,7 +655,7 @@ __global__ __launch_bounds__(kBlock, XRT_DEEP_WAVES) void k_trace_deep4q(KParams
             if (!active) {
                 const uint32_t idx = b + (uint32_t)__popcll(idle & ((1ull << (lane & ~3)) - 1ull));
                 if (idx < cnt) {
-                    const uint32_t e = dq[idx];
+                    const uint32_t e = idx < n_ext ? dq[idx] : dqs[idx];
                     s = e >> 3;
                     const uint32_t kind = e & 7u;
                     any = kind != 0;
@@ -2644,7 +2653,7 @@ hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* 
         const bool nl1 = P.n_lights <= 1;
         if (P.two_level) {
             if (!P.deep || !P.deep_count) return hipErrorInvalidValue;
-            hipError_t e = hipMemsetAsync(P.deep_count, 0, 2 * kMaxParts * sizeof(uint32_t), st);   // counts, fetch counters
+            hipError_t e = hipMemsetAsync(P.deep_count, 0, 3 * kMaxParts * sizeof(uint32_t), st);   // counts, fetch counters
             if (e != hipSuccess) return e;
             const size_t lds_a = (size_t)P.n_stri * 3 * sizeof(f4) + (size_t)P.n_sobj * (sizeof(DObjBox) + sizeof(DObjPlane));
             if (P.sstep)

@@ -125,7 +125,7 @@ int setup_deep(xrt_ctx* c, KParams& P) {
     P.deep = nullptr, P.deep_count = nullptr, P.deep_cap = 0;
     if (!P.two_level) return XRT_OK;
     P.deep_cap = P.part_cap * (1u + (uint32_t)P.n_lights);
-    const size_t words = (size_t)P.n_part * P.deep_cap + 2 * kMaxParts;   // queues, counts, fetch counters
+    const size_t words = (size_t)P.n_part * P.deep_cap + 3 * kMaxParts;   // queues, counts, fetch counters
     const int rc = ensure(c, c->deep, words * 4);
     if (rc) return rc;
     P.deep = as<uint32_t>(c->deep);
