@@ -28,6 +28,14 @@ def compare(img, ref):
     assert len(bad) == 0, (len(bad), bad[:5], rmse)
 
 
+def partitions(n_slots, merged=False):
+    """The library's live-list partition count for a shard of n_slots (xrt_api.cpp): the merged
+    schedule takes >= 2048 slots per partition (at most 256), the others >= 512 (at most 1024)."""
+    max_parts, min_slots = (256, 2048) if merged else (1024, 512)
+    n = min(max_parts, max(1, n_slots // min_slots))
+    return n & ~7 if n >= 8 else n
+
+
 def counters_equal(g, st):
     assert (g.segments, g.shadow_rays, g.draws, g.rejected, g.stalled) == \
         (st["segments"], st["shadow_rays"], st["draws"], st["rejected"], st["stalled"])
@@ -60,11 +68,11 @@ def render_like_bench(r, cfg, spp):
 
 def test_c2_headline_geometry(renderer):
     """C2 (Cornell 800x600, GI(3)): the headline kernel k_step_merged with full waves (64
-    slots per wave, pair passes, no group traces) over 64 live-list partitions, 64
+    slots per wave, pair passes, no group traces) over 232 live-list partitions, 64
     segments per launch — the instantiation the bench's number comes from."""
     img, ref, st, g = render_like_bench(renderer, "C2", 4)
     assert g.schedule == abi.XRT_SCHED_STEP_MERGED
-    assert (g.slots_per_wave, g.group_lanes, g.partitions, g.visits_per_launch) == (64, 1, 64, 64)
+    assert (g.slots_per_wave, g.group_lanes, g.partitions, g.visits_per_launch) == (64, 1, partitions(480000, merged=True), 64)
     assert g.samples == 800 * 600 * 4
     compare(img, ref)
     counters_equal(g, st)
@@ -79,7 +87,7 @@ def test_c2_headline_across_launches(renderer):
     Full frame, bit-exact, counters equal (Src/renderer.cpp:29-81, Src/sampler.h:16-50)."""
     img, ref, st, g = render_like_bench(renderer, "C2", 64)
     assert g.schedule == abi.XRT_SCHED_STEP_MERGED
-    assert (g.slots_per_wave, g.group_lanes, g.partitions, g.visits_per_launch) == (64, 1, 64, 64)
+    assert (g.slots_per_wave, g.group_lanes, g.partitions, g.visits_per_launch) == (64, 1, partitions(480000, merged=True), 64)
     assert g.launches[abi.XRT_K_STEP] >= 3, g.launches[abi.XRT_K_STEP]
     assert g.launches[abi.XRT_K_REFILL] == 1    # only the first twist of every slot is a launch
     # in-launch refills ran (measured: 258,950 for 480,000 slots — pixels whose samples end
@@ -106,7 +114,7 @@ def test_c3_geometry_across_launches(renderer):
                            timing=True, schedule="auto")
     g = renderer.stats
     img = fb.cpu().numpy()
-    assert g.schedule == abi.XRT_SCHED_STEP and g.partitions == 64
+    assert g.schedule == abi.XRT_SCHED_STEP and g.partitions == partitions(w * h)
     assert g.launches[abi.XRT_K_STEP] >= 3 and g.launches[abi.XRT_K_REFILL] >= 2, list(g.launches)
     assert g.rng_twists > g.path_slots
     assert g.segments == w * h * spp   # Direct: one Scene::intersect per sample
@@ -117,10 +125,10 @@ def test_c3_geometry_across_launches(renderer):
 
 def test_c3_geometry(renderer):
     """C3 (1,000 spheres + sphere light, 1280x720, Direct): fused k_step with the LDS
-    skip-link sphere BVH, 64 partitions."""
+    skip-link sphere BVH, 1024 partitions."""
     img, ref, st, g = render_like_bench(renderer, "C3", 1)
     assert g.schedule == abi.XRT_SCHED_STEP
-    assert g.partitions == 64
+    assert g.partitions == partitions(1280 * 720)
     compare(img, ref)
     counters_equal(g, st)
 

@@ -26,6 +26,7 @@ def main():
     group = "--no-group" not in sys.argv
     cfg = scenes.CONFIGS[cfg_name]
     W, H, SPP = cfg["width"], cfg["height"], cfg["spp"]
+    SPP = ([int(a.split("=")[1]) for a in sys.argv if a.startswith("--spp=")] or [SPP])[0]
     scene = scenes.build(cfg_name)
     r = HipRenderer(SPP, device=0)
     r.upload(scene)

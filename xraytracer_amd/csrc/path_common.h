@@ -299,7 +299,8 @@ __device__ __forceinline__ PartIter part_iter(const KParams& P, const uint32_t* 
     return it;
 }
 __device__ __forceinline__ void zero_parts(const KParams& P, uint32_t* c) {
-    if (blockIdx.x == 0 && threadIdx.x < P.n_part) c[threadIdx.x] = 0;
+    if (blockIdx.x == 0)
+        for (uint32_t i = threadIdx.x; i < P.n_part; i += kBlock) c[i] = 0;
 }
 
 

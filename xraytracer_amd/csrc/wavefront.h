@@ -30,7 +30,14 @@ constexpr uint32_t kRngMin = 64;     // request a refill when fewer words than t
 constexpr uint32_t kRngVisit = 16;   // a slot visit needs at least this many (max draws of a
                                      // GI/Direct visit with kMaxLights lights is 13; VPT walks
                                      // suspend themselves below 8)
-constexpr uint32_t kMaxParts = 64;   // live-list partitions (counters per list)
+#ifndef XRT_MAX_PARTS
+#define XRT_MAX_PARTS 1024
+#endif
+#ifndef XRT_PART_MIN
+#define XRT_PART_MIN 512
+#endif
+constexpr uint32_t kMaxParts = XRT_MAX_PARTS;   // live-list partitions (counters per list)
+constexpr uint32_t kPartMinSlots = XRT_PART_MIN;   // ... of at least this many slots each
 constexpr uint32_t kStepVisits = 32; // fused schedule: path segments per slot per k_step
 constexpr uint32_t kMergedVisits = 64; // merged-trace schedule: segments per slot per launch (at most;
                                        // clamped so a launch's draws fit one refill block)

@@ -74,13 +74,15 @@ __global__ __launch_bounds__(kBlock) void k_seed(KParams P, uint32_t* list, uint
         P.c_stall[s] = 0;
         list[s] = s;
     }
-    if (blockIdx.x == 0 && threadIdx.x < P.n_part) {
-        const uint32_t p = threadIdx.x, lo = p * P.part_cap;
-        const uint32_t c = lo < P.n_slots ? min(P.part_cap, P.n_slots - lo) : 0u;
-        count[p] = c;
-        count_other[p] = 0;
-        req_count[p] = c;
-        req_count[kMaxParts + p] = 0;
+    if (blockIdx.x == 0) {
+        for (uint32_t p = threadIdx.x; p < P.n_part; p += kBlock) {
+            const uint32_t lo = p * P.part_cap;
+            const uint32_t c = lo < P.n_slots ? min(P.part_cap, P.n_slots - lo) : 0u;
+            count[p] = c;
+            count_other[p] = 0;
+            req_count[p] = c;
+            req_count[kMaxParts + p] = 0;
+        }
     }
 }
 
