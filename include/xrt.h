@@ -133,8 +133,8 @@ enum {
     XRT_FLAG_NO_GROUP = 8u,    /* merged schedule with 16/32 slots per wave: spread the traces
                                   over idle lanes (pair passes) instead of 4/2-lane groups    */
     XRT_FLAG_DEEP_SINGLE = 32u, /* two-level traces: walk the BVH with one lane per queued ray  */
-    XRT_FLAG_DEEP_QUAD = 64u,   /* ... with four lanes per ray (default: four below 1.5M slots);
-                                   results never depend on either                              */
+    XRT_FLAG_DEEP_QUAD = 64u,   /* ... with four lanes per ray (the default); results never
+                                   depend on either                                            */
     XRT_FLAG_ACCUMULATE = 16u  /* Renderer::render's in-place contract (Src/renderer.cpp:75,98):
                                   each owned pixel starts from the value already in the output
                                   buffer (Image::addPixel adds to it in sample order), then

@@ -137,8 +137,8 @@ def test_c3_geometry(renderer):
 def test_c4_mesh_geometry(renderer, deep):
     """C4's own mesh: SphereMesh(nTheta = nPhi = 160) = 51,200 triangles + the Cornell box
     (51,236), at C4's 16:9 aspect (160x90): wavefront schedule with the two-level trace, the
-    BVH walked with four lanes per queued ray (what row shards run) and with one (what the
-    full 1920x1080 frame runs, above 1.5M path slots)."""
+    BVH walked with four lanes per queued ray (the default, what the bench runs) and with
+    one (XRT_FLAG_DEEP_SINGLE)."""
     s = scenes.cornell_spheremesh(160, 90)
     assert s.desc.n_tris == 51200 + 36
     renderer.spp = 2

@@ -24,6 +24,7 @@ def main():
     only = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--only=")]
     spw = ([int(a.split("=")[1]) for a in sys.argv if a.startswith("--spw=")] or [0])[0]
     group = "--no-group" not in sys.argv
+    deep = ([a.split("=")[1] for a in sys.argv if a.startswith("--deep=")] or ["auto"])[0]
     cfg = scenes.CONFIGS[cfg_name]
     W, H, SPP = cfg["width"], cfg["height"], cfg["spp"]
     SPP = ([int(a.split("=")[1]) for a in sys.argv if a.startswith("--spp=")] or [SPP])[0]
@@ -39,7 +40,7 @@ def main():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             st = r.render_device(scene, W, H, fb.data_ptr(), shard_index=s, shard_count=n, timing=timing,
-                                 slots_per_wave=spw, group=group)
+                                 slots_per_wave=spw, group=group, deep=deep)
             torch.cuda.synchronize()
             times.append(time.perf_counter() - t0)
         slow = max(times)

@@ -261,6 +261,14 @@ __device__ __forceinline__ uint64_t min64_dpp(uint64_t x) {
     return y < x ? y : x;
 }
 template <int G>
+__device__ __forceinline__ uint32_t group_min32(uint32_t x) {
+    if (G >= 2) x = min(x, dpp32<0xB1>(x));
+    if (G >= 4) x = min(x, dpp32<0x4E>(x));
+    if (G >= 8) x = min(x, dpp32<0x141>(x));
+    if (G >= 16) x = min(x, dpp32<0x140>(x));
+    return x;
+}
+template <int G>
 __device__ __forceinline__ uint64_t group_min64(uint64_t x) {
     if (G >= 2) x = min64_dpp<0xB1>(x);
     if (G >= 4) x = min64_dpp<0x4E>(x);

@@ -610,17 +610,20 @@ __global__ __launch_bounds__(kBlock, XRT_DEEP_WAVES) void k_trace_deep4(KParams 
 }
 
 // Phase B with four lanes per ray ("quad"): lane q of a quad owns child q of the current
-// node — loads its two float4, tests its box and, for a leaf child, that leaf's triangles —
-// and the quad combines by DPP quad_perm: the closest hit as the minimum of (t bits, index
-// + 1) (the lexicographic (t, index) order of bvh_leaf's update; a lane that found nothing
-// better still holds the ray's current hit), occlusion as an or, the next node as the
-// nearest overlapping interior child (ties to the lower child) with the other overlapping
-// ones pushed.  A step costs one node fetch and at most one leaf's tests per lane instead of
-// four boxes and up to four leaves, so the longest walk of a launch — which bounds the
+// node — loads its two float4, tests its box and, for a leaf child, that leaf's triangles.
+// Each lane keeps its own best hit over the triangles it tested (bvh_leaf's (t, index) update
+// from the ray's phase-A hit), and the quad shares only what steers the walk, by DPP
+// quad_perm: the smallest t as the pruning limit (a 32-bit min per step), occlusion as an or,
+// and the next node — the nearest overlapping interior child (key: entry distance with its
+// two low bits replaced by the child slot; the order only steers the walk) — with the other
+// overlapping ones pushed on one stack per quad.  When the walk ends the quad's closest hit
+// is the minimum of the lanes' (t bits, index + 1) keys and the lane holding it writes its
+// own (t, u, v, index).  A step costs one node fetch and at most one leaf per lane instead
+// of four boxes and up to four leaves, so the longest walk of a launch — which bounds the
 // launch when few rays are queued (a row shard of a multi-GPU frame) — takes fewer cycles.
 // Exact for the same reason as k_trace_deep4: every triangle whose padded box overlaps
-// [0, best t] is tested, whatever the order.  Rays are fetched a quad at a time with the
-// same partitioned queue and counters.
+// [0, best t] is tested by some lane (each lane's limit is at least the quad's best t).
+// Rays are fetched a quad at a time from the same partitioned queues and counters.
 template <typename SE>
 __global__ __launch_bounds__(kBlock, XRT_DEEP_WAVES) void k_trace_deep4q(KParams P) {
     extern __shared__ uint32_t bvh_stack_lds[];
@@ -681,36 +684,30 @@ __global__ __launch_bounds__(kBlock, XRT_DEEP_WAVES) void k_trace_deep4q(KParams
         }
         if (!__ballot(active)) break;
         if (!active) continue;
-        // ---- one node: child q on lane q
+        // ---- one node: child q on lane q; lim = the quad's best t (closest hits) or tmax
         const f4* N = node < ntop ? top + 8 * node : P.bvh4 + 8 * (size_t)node;
         const f4 lo = N[q], hi = N[4 + q];
         const int cidx = __float_as_int(lo.w), ccnt = __float_as_int(hi.w);
-        const float e = ccnt >= 0 ? bvh_enter(lo, hi, o, inv, any ? tmax : bt) : __builtin_inff();
-        bool done;
+        float lim = any ? tmax : __uint_as_float(group_min32<4>(__float_as_uint(bt)));   // t >= 0: bits order
+        const float e = ccnt >= 0 ? bvh_enter(lo, hi, o, inv, lim) : __builtin_inff();
+        bool done = false;
         if (any) {
             bool occ = false;
             if (ccnt > 0 && e != __builtin_inff()) occ = bvh_leaf_batch<true>(P, cidx, ccnt, o, d, tmax, bt, bu, bv, bk);
             done = group_or32<4>(occ ? 1u : 0u) != 0u;
             if (done && q == 0) atomicOr(P.occ + s, 1u << l);
         } else {
-            float t1 = bt, u1 = bu, v1 = bv;
-            int k1 = bk;
-            if (ccnt > 0 && e != __builtin_inff()) (void)bvh_leaf_batch<false>(P, cidx, ccnt, o, d, kINF, t1, u1, v1, k1);
-            const uint64_t key = ((uint64_t)__float_as_uint(t1) << 32) | (uint32_t)(k1 + 1);
-            const uint64_t kmin = group_min64<4>(key);
-            const bool win = key == kmin;   // lanes holding the minimum hold the same (u, v)
-            bu = __uint_as_float(group_or32<4>(win ? __float_as_uint(u1) : 0u));
-            bv = __uint_as_float(group_or32<4>(win ? __float_as_uint(v1) : 0u));
-            bt = __uint_as_float((uint32_t)(kmin >> 32));
-            bk = (int)(uint32_t)kmin - 1;
-            done = false;
+            if (ccnt > 0 && e != __builtin_inff()) {
+                (void)bvh_leaf_batch<false>(P, cidx, ccnt, o, d, kINF, bt, bu, bv, bk);
+                lim = __builtin_fminf(lim, bt);   // this lane's leaf may have closed in
+            }
+            lim = __uint_as_float(group_min32<4>(__float_as_uint(lim)));
         }
         if (!done) {
-            const float lim = any ? tmax : bt;
             const bool inner = ccnt == 0 && e <= lim;   // interior child still overlapping [0, lim]
-            const uint64_t nkey = inner ? (((uint64_t)__float_as_uint(e) << 32) | (uint32_t)q) : ~0ull;
-            const uint64_t nmin = group_min64<4>(nkey);
-            if (nmin != ~0ull) {
+            const uint32_t nkey = inner ? ((__float_as_uint(e) & ~3u) | (uint32_t)q) : ~0u;
+            const uint32_t nmin = group_min32<4>(nkey);
+            if (nmin != ~0u) {
                 const bool nearest = nkey == nmin;
                 const uint32_t m4 = (uint32_t)(__ballot(inner && !nearest) >> (lane & ~3)) & 0xfu;
                 if (inner && !nearest) stk[(sp + __popc(m4 & ((1u << q) - 1u))) * kQuads] = (SE)cidx;
@@ -723,7 +720,12 @@ __global__ __launch_bounds__(kBlock, XRT_DEEP_WAVES) void k_trace_deep4q(KParams
             }
         }
         if (done) {
-            if (!any && q == 0) P.hit[s] = make_float4(bt, bu, bv, __int_as_float(bk));
+            if (!any) {   // the quad's closest hit: the smallest (t bits, index + 1) of the lanes
+                const uint64_t key = ((uint64_t)__float_as_uint(bt) << 32) | (uint32_t)(bk + 1);
+                const uint64_t kmin = group_min64<4>(key);
+                const uint32_t wm = (uint32_t)(__ballot(key == kmin) >> (lane & ~3)) & 0xfu;
+                if (q == __builtin_ctz(wm)) P.hit[s] = make_float4(bt, bu, bv, __int_as_float(bk));
+            }
             active = false;
         }
     }
