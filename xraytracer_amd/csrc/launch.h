@@ -22,8 +22,10 @@ hipError_t launch_seed(const KParams& P, uint32_t* list, uint32_t* count, uint32
 hipError_t launch_refill(const KParams& P, const uint32_t* count, uint32_t* zero_count, hipStream_t st);
 hipError_t launch_trace_2a_coop(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
                                 uint32_t blocks, hipStream_t st);
+// zero_deep: clear the two-level trace's queue counters first (false when the k_shade that
+// precedes this trace in the render loop has cleared them)
 hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
-                        uint32_t blocks, hipStream_t st);
+                        uint32_t blocks, hipStream_t st, bool zero_deep = true);
 // phase B of a two-level trace (the BVH walk of the rays launch_trace queued); no-op otherwise
 hipError_t launch_trace_deep(const KParams& P, hipStream_t st);
 hipError_t launch_shade(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,

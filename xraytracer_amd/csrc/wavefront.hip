@@ -1133,6 +1133,10 @@ __global__ __launch_bounds__(kBlock, XRT_SHADE_WAVES) void k_shade(KParams P, co
     __shared__ __attribute__((aligned(16))) uint32_t rbuf[kBlock / 64][kMT];   // wave_refill staging
     const PartIter it = part_iter(P, count, kBlock);
     const int tid = threadIdx.x, lane = tid & 63;
+    // the two-level trace that follows appends to zeroed deep-queue counters (instead of a
+    // memset launch per iteration); the previous iteration's deep walk is done by now
+    if (P.two_level && P.deep_count && blockIdx.x == 0)
+        for (uint32_t q = tid; q < 3 * kMaxParts; q += kBlock) P.deep_count[q] = 0;
     for (uint32_t base = it.first; base < it.n; base += it.stride) {
         const uint32_t i = base + tid;
         const bool valid = i < it.n;
@@ -2647,7 +2651,7 @@ hipError_t launch_trace_deep(const KParams& P, hipStream_t st) {
 }
 
 hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* zero,
-                        uint32_t blocks, hipStream_t st) {
+                        uint32_t blocks, hipStream_t st, bool zero_deep) {
     if (P.bvh_node && P.scene_kind == SCN_TRI) {
         if (P.bvh_stack <= 0 || P.bvh_stack > kBvhStack) return hipErrorInvalidValue;
         // node indices below 2^16: 16-bit stack entries, half the LDS per thread
@@ -2657,7 +2661,8 @@ hipError_t launch_trace(const KParams& P, const uint32_t* list, const uint32_t* 
         const bool nl1 = P.n_lights <= 1;
         if (P.two_level) {
             if (!P.deep || !P.deep_count) return hipErrorInvalidValue;
-            hipError_t e = hipMemsetAsync(P.deep_count, 0, 3 * kMaxParts * sizeof(uint32_t), st);   // counts, fetch counters
+            hipError_t e = zero_deep ? hipMemsetAsync(P.deep_count, 0, 3 * kMaxParts * sizeof(uint32_t), st)   // counts,
+                                     : hipSuccess;                                                        // fetch counters
             if (e != hipSuccess) return e;
             const size_t lds_a = (size_t)P.n_stri * 3 * sizeof(f4) + (size_t)P.n_sobj * (sizeof(DObjBox) + sizeof(DObjPlane));
             if (P.sstep)

@@ -938,7 +938,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             });
             if (e != hipSuccess) return hip_err(c, e, "k_shade");
             e = launch(XRT_K_TRACE, [&] {
-                return launch_trace(P, lists[nxt], counts_at(nxt), counts_at(cur), blocks, c->stream);
+                return launch_trace(P, lists[nxt], counts_at(nxt), counts_at(cur), blocks, c->stream, false);
             });
             if (e != hipSuccess) return hip_err(c, e, "k_trace");
             if (P.two_level && P.bvh_node && P.scene_kind == SCN_TRI) {
