@@ -29,6 +29,8 @@ def main():
     W, H, SPP = cfg["width"], cfg["height"], cfg["spp"]
     SPP = ([int(a.split("=")[1]) for a in sys.argv if a.startswith("--spp=")] or [SPP])[0]
     scene = scenes.build(cfg_name)
+    if "--sparse" in sys.argv:   # media: upload the grid as 8^3 leaf bricks (same image)
+        scene.medium.sparse = True
     r = HipRenderer(SPP, device=0)
     r.upload(scene)
     fb = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0")
