@@ -405,6 +405,20 @@ def test_vpt_medium_walk_suspends_and_resumes(renderer, sched):
     assert renderer.stats.draws == st["draws"]
 
 
+@pytest.mark.parametrize("visits", [1, 3, 128])
+@pytest.mark.parametrize("integ", ["vpt", "vpt_nee"])
+def test_vpt_events_resume_across_launches(renderer, visits, integ):
+    """The fused VPT kernel runs one event (a trace or ONE collision) per iteration and a walk
+    carries over in registers; with 1-3 events per launch almost every walk is saved at a
+    launch end and resumed by the next launch.  Bit-exact, same draws and segments."""
+    s = dense_smoke(20, 15) if integ == "vpt_nee" else scenes.smoke(20, 15, n=32)
+    img, ref, st = render_both(renderer, s, 20, 15, 6, integrator=integ, visits_per_launch=visits)
+    compare(img, ref)
+    g = renderer.stats
+    assert g.visits_per_launch == visits
+    assert g.draws == st["draws"] and g.segments == st["segments"]
+
+
 def dense_smoke(w, h, n=24, g=0.4):
     """Smoke scene with a denser, anisotropic medium: more scattering events, more NEE ratio
     tracking steps per light sample, HenyeyGreenstein with g != 0."""

@@ -50,6 +50,23 @@ constexpr uint32_t kMergedLive32 = XRT_LIVE32;   // ... and for 32 (below: 16 sl
 #define XRT_LIVE16 20000
 #endif
 constexpr uint32_t kMergedLive16 = XRT_LIVE16;   // ... and for 16 (below: 4 slots, 16 lanes each)
+#ifndef XRT_VPT_EVENTS
+#define XRT_VPT_EVENTS 1
+#endif
+constexpr bool kVptEvents = XRT_VPT_EVENTS != 0;   // VPT k_step: one event (trace or collision) per iteration
+#ifndef XRT_VPT_EV_VISITS
+#define XRT_VPT_EV_VISITS 128
+#endif
+#ifndef XRT_VPT_EV_DRAWS
+#define XRT_VPT_EV_DRAWS 4
+#endif
+#ifndef XRT_VPT_EV_PF
+#define XRT_VPT_EV_PF 4
+#endif
+constexpr uint32_t kVptEventVisits = XRT_VPT_EV_VISITS;   // ... events per slot per launch
+constexpr uint32_t kVptEventDraws = XRT_VPT_EV_DRAWS;     // ... draws of an event for the refill threshold (a
+                                           // collision draws <= 5; a lane with fewer words left stops early)
+constexpr uint32_t kVptEventPrefetch = XRT_VPT_EV_PF;     // ... reload the 8-word RNG window below this many
 constexpr uint32_t kStepRefill = 1;  // fused schedule: k_refill after every k_step
 constexpr uint32_t kVisitDraws = 13; // max RNG draws of one GI/Direct segment (4 lights)
 // fused schedule: a slot queues a refill when fewer than refill * visits * 13 + kRngVisit

@@ -1846,10 +1846,21 @@ __global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, con
         float* px = P.fb + 3 * ((size_t)col + (size_t)P.width * row);
         v3 acc = mk(px[0], px[1], px[2]);   // the pixel's running sum, in registers this launch
         rng.prefetch(g - rng.c);
+        // VPT family: one event per iteration (kVptEvents) — a trace + surface interaction, or
+        // ONE delta-tracking collision of a walk that continues across iterations in
+        // registers — so lanes whose walks end early start their next segment (or sample)
+        // while the others keep colliding, instead of idling until the wave's longest walk
+        // ends.  Each lane's own sequence of operations and draws is unchanged.
+        constexpr bool EV = vpt_family(INTEG) && kVptEvents;
+        bool walking = false;
+        float mt = 0.0f, mt1 = 0.0f;
+        v3 tt = mk(1, 1, 1), sa = mk(0, 0, 0);
         for (uint32_t vis = 0; vis < visits; ++vis) {
-            if ((st & ST_DONE) || g - rng.c < kRngVisit) break;
+            if ((st & ST_DONE) || (!walking && g - rng.c < kRngVisit)) break;
             bool ended = false, trace = true;
-            if (st & ST_REGEN) {
+            if (EV && walking) {
+                trace = false;
+            } else if (st & ST_REGEN) {
                 // next sample: jitter draws + camera ray (Src/renderer.cpp:44-50)
                 st &= ~ST_REGEN;
                 const float u = div_w(P, (float)(int)col + rng.next());
@@ -1869,9 +1880,8 @@ __global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, con
                     else trace = true;
                 }
             }
-            bool walk = false;
-            float mt = 0.0f, mt1 = 0.0f;
-            v3 tt = mk(1, 1, 1), sa = mk(0, 0, 0);
+            bool walk = EV && walking;
+            if (!walk) mt = 0.0f, mt1 = 0.0f, tt = mk(1, 1, 1), sa = mk(0, 0, 0);
             if (vpt_family(INTEG) && (st & ST_MEDIUM)) {
                 st &= ~ST_MEDIUM;
                 const f4 m1 = P.med[s], m2 = P.med2[s];
@@ -1997,10 +2007,13 @@ __global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, con
             }
             if (vpt_family(INTEG) && walk) {
                 v3 pos, dir, tm;
-                const int r = P.medium.kind == XRT_MEDIUM_HETEROGENEOUS
-                                  ? delta_track(P, o, d, thr, mt, mt1, tt, sa, rng, g, pos, dir, tm)
-                                  : homog_track(P, o, d, thr, mt, mt1, rng, pos, dir, tm);
-                if (r == 2) {
+                const int r = P.medium.kind != XRT_MEDIUM_HETEROGENEOUS
+                                  ? homog_track(P, o, d, thr, mt, mt1, rng, pos, dir, tm)
+                              : EV ? delta_step(P, o, d, thr, mt, mt1, tt, sa, rng, g, pos, dir, tm)
+                                   : delta_track(P, o, d, thr, mt, mt1, tt, sa, rng, g, pos, dir, tm);
+                walking = EV && r == 3;   // null collision: the walk goes on next iteration
+                if (r == 3) {
+                } else if (r == 2) {
                     st |= ST_MEDIUM;
                     P.med[s] = make_float4(mt, mt1, sa.x, sa.y);
                     P.med2[s] = make_float4(tt.x, tt.y, tt.z, sa.z);
@@ -2045,7 +2058,12 @@ __global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, con
                     depth = 0;
                 }
             }
-            rng.prefetch(g - rng.c);
+            if (!EV || rng.nb < kVptEventPrefetch) rng.prefetch(g - rng.c);
+        }
+        if (EV && walking) {   // the launch ended mid-walk: resume it like a suspended one
+            st |= ST_MEDIUM;
+            P.med[s] = make_float4(mt, mt1, sa.x, sa.y);
+            P.med2[s] = make_float4(tt.x, tt.y, tt.z, sa.z);
         }
         px[0] = acc.x, px[1] = acc.y, px[2] = acc.z;
         // queue an RNG refill for k_refill (words ahead < rng_keep, once per request)

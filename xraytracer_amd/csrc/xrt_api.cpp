@@ -880,6 +880,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     const uint32_t step_visits = ev                    ? (uint32_t)std::atoi(ev)
                                  : p->visits_per_launch ? p->visits_per_launch
                                  : merged               ? merged_visits
+                                 : (volumetric && kVptEvents) ? kVptEventVisits
                                                         : kStepVisits;
     // the merged kernel relies on one refill launch after every step launch (it clears
     // ST_RNGREQ itself)
@@ -887,8 +888,9 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     merged_refill = merged;
     // a slot queues a refill when fewer words are left than the next `refill` launches can
     // draw: the merged kernel draws at most step_merged_draws per segment and checks it
-    P.rng_keep = merged ? step_refill * step_visits * step_merged_draws(P) + step_merged_draws(P)
-                        : step_refill * step_visits * kVisitDraws + kRngVisit;
+    P.rng_keep = merged                      ? step_refill * step_visits * step_merged_draws(P) + step_merged_draws(P)
+                 : (volumetric && kVptEvents) ? step_refill * step_visits * kVptEventDraws + kRngVisit
+                                              : step_refill * step_visits * kVisitDraws + kRngVisit;
     if (P.rng_keep > kMT) return set_err(c, XRT_ERR_INVALID, "visits_per_launch too large for the RNG ring");
     // device copy of the (now final) parameters for kernels that read them from memory
     if ((rc = ensure(c, c->kparams, sizeof(KParams)))) return rc;
