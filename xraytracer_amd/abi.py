@@ -13,8 +13,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libxrt_hip.so")
-if os.environ.get("XRT_LIB"):   # experiment builds (csrc/Makefile `variant`), same ABI
-    LIB_PATH = os.path.join(HERE, os.environ["XRT_LIB"])
+if os.environ.get("XRT_LIB"):   # experiment builds (csrc/Makefile `variant` -> variants/), same ABI
+    _v = os.path.join(HERE, "variants", os.environ["XRT_LIB"])
+    LIB_PATH = _v if os.path.exists(_v) else os.path.join(HERE, os.environ["XRT_LIB"])
 
 XRT_ABI_VERSION = 9   # include/xrt.h XRT_ABI_VERSION
 XRT_OK = 0
