@@ -643,6 +643,10 @@ __global__ __launch_bounds__(kBlock, XRT_DEEP_WAVES) void k_trace_deep4q(KParams
     const uint32_t* dq = P.deep + (size_t)p * P.deep_cap;
     const uint32_t* dqs = dq + P.part_cap - n_ext;   // dqs[idx] for idx >= n_ext
     constexpr uint64_t kLeads = 0x1111111111111111ull;   // lane 0 of every quad
+#ifdef XRT_EXPERIMENTS
+    if (blockIdx.x < P.n_part && tid == 0) atomicAdd(P.stats + 38, (unsigned long long)cnt);
+    uint32_t nsteps = 0, niter = 0;
+#endif
     bool active = false, drained = cnt == 0, any = false;
     uint32_t s = 0, l = 0;
     int node = 0, sp = 0, bk = -1;
@@ -683,6 +687,10 @@ __global__ __launch_bounds__(kBlock, XRT_DEEP_WAVES) void k_trace_deep4q(KParams
             }
         }
         if (!__ballot(active)) break;
+#ifdef XRT_EXPERIMENTS
+        ++niter;
+        nsteps += (uint32_t)__popcll(__ballot(active) & kLeads);   // quads stepping (wave-uniform)
+#endif
         if (!active) continue;
         // ---- one node: child q on lane q; lim = the quad's best t (closest hits) or tmax
         const f4* N = node < ntop ? top + 8 * node : P.bvh4 + 8 * (size_t)node;
@@ -729,6 +737,11 @@ __global__ __launch_bounds__(kBlock, XRT_DEEP_WAVES) void k_trace_deep4q(KParams
             active = false;
         }
     }
+#ifdef XRT_EXPERIMENTS
+    if (lane == 0)
+        atomicAdd(P.stats + 39, (unsigned long long)nsteps), atomicAdd(P.stats + 37, (unsigned long long)niter),
+            atomicMax(P.stats + 36, (unsigned long long)niter);
+#endif
 }
 
 // Small triangle scenes (<= kSmallTris triangles, e.g. the Cornell box): every triangle
