@@ -172,6 +172,10 @@ struct DMedium {
     const int* brick_table;
     const float* bricks;
     int nbx, nby, nbz;
+    // dense grid: every cell's eight corner values in BoxSampler's order (d000 d001 d010 d011
+    // d100 d101 d110 d111), 32 B per cell [(k * (ny-1) + j) * (nx-1) + i], so an interior
+    // lookup is one 32-byte load instead of four rows of the grid; null when not built
+    const float* corners;
 };
 
 #ifdef __HIPCC__

@@ -862,6 +862,13 @@ __device__ __forceinline__ bool dense_interior(const DMedium& M, const VdbCell& 
     return !M.brick_table && C.i >= 0 && C.j >= 0 && C.k >= 0 && C.i + 1 < M.nx && C.j + 1 < M.ny && C.k + 1 < M.nz;
 }
 __device__ __forceinline__ void dense_corners(const DMedium& M, const VdbCell& C, float (&q)[8]) {
+    if (M.corners) {
+        const f4* r = reinterpret_cast<const f4*>(M.corners) +
+                      2 * (((size_t)C.k * (M.ny - 1) + (size_t)C.j) * (M.nx - 1) + (size_t)C.i);
+        const f4 a = r[0], b = r[1];
+        q[0] = a.x, q[1] = a.y, q[2] = a.z, q[3] = a.w, q[4] = b.x, q[5] = b.y, q[6] = b.z, q[7] = b.w;
+        return;
+    }
     typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
     using g2 = __attribute__((address_space(1))) const f2u;
     const float* b = M.density + ((size_t)C.k * M.ny + (size_t)C.j) * M.nx + (size_t)C.i;

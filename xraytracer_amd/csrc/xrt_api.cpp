@@ -66,6 +66,7 @@ struct xrt_ctx {
     std::vector<int> obj_tri_first;
     DevBuf q_rays, q_tmax, q_out;
     DevBuf brick_table, brick_data;   // sparse medium (xrt_set_medium_bricks)
+    DevBuf corners;                   // dense medium: per-cell corner values (DMedium::corners)
     DevBuf stage;              // multi: device-output staging on subs[0] (accumulate from a device image)
 };
 
@@ -243,7 +244,7 @@ void xrt_destroy(xrt_ctx* c) {
     for (DevBuf* b : all) free_buf(*b);
     free_buf(c->stri), free_buf(c->sbox), free_buf(c->splane), free_buf(c->bvh4), free_buf(c->deep);
     free_buf(c->stage), free_buf(c->q_rays), free_buf(c->q_tmax), free_buf(c->q_out);
-    free_buf(c->brick_table), free_buf(c->brick_data);
+    free_buf(c->brick_table), free_buf(c->brick_data), free_buf(c->corners);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->poll_ev)
         if (e) (void)hipEventDestroy(e);
@@ -617,6 +618,28 @@ static int set_medium_one(xrt_ctx* c, const xrt_medium_desc* m) {
     DMedium& D = c->base.medium;
     D = DMedium{};
     D.density = as<float>(c->density);
+#ifndef XRT_CORNER_GRID
+#define XRT_CORNER_GRID 1
+#endif
+    // the per-cell corner layout (8x the grid's bytes; skipped above 2 GiB)
+    const size_t cx = m->nx - 1, cy = m->ny - 1, cz = m->nz - 1, cells = cx * cy * cz;
+    if (XRT_CORNER_GRID && cells && cells * 32 <= (size_t(2) << 30)) {
+        std::vector<float> cor(cells * 8);
+        const float* g = m->density;
+        const size_t sy = m->nx, sz = (size_t)m->nx * m->ny;
+        for (size_t k = 0; k < cz; ++k)
+            for (size_t j = 0; j < cy; ++j)
+                for (size_t i = 0; i < cx; ++i) {
+                    const float* b = g + k * sz + j * sy + i;
+                    float* o = cor.data() + 8 * ((k * cy + j) * cx + i);
+                    o[0] = b[0], o[1] = b[sz], o[2] = b[sy], o[3] = b[sy + sz];
+                    o[4] = b[1], o[5] = b[1 + sz], o[6] = b[1 + sy], o[7] = b[1 + sy + sz];
+                }
+        if ((rc = upload(c, c->corners, cor.data(), cor.size() * sizeof(float)))) return rc;
+        D.corners = as<float>(c->corners);
+    } else {
+        free_buf(c->corners);
+    }
     return set_medium_grid(c, m);
 }
 
