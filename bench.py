@@ -2,9 +2,11 @@
 
 One step = one full frame of the workload (default C2: Cornell box 800x600, 1024 spp,
 GIIntegrator(3)), rendered by the MI355X wavefront through libxrt_hip.so with the scene
-already resident in HBM.  With N GPUs (one process per GPU, torchrun) each rank renders the
-rows y % N == rank and the float3 framebuffers are summed to rank 0 with an RCCL reduce
-(exact: the other ranks contribute zeros).  Total work is fixed as N grows: "strong".
+already resident in HBM.  With N GPUs (one process per GPU) each rank renders the rows
+y % N == rank and the float3 framebuffers are summed to rank 0 with an RCCL reduce (exact:
+the other ranks contribute zeros).  Total work is fixed as N grows: "strong".  Under torchrun
+WORLD_SIZE must equal N; without a launcher and N > 1 the bench starts N ranks itself
+(torch.distributed.run, child process); it exits non-zero rather than render N > 1 on one GPU.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--no-cpu]
 """
@@ -90,6 +92,48 @@ def cpu_baseline(cfg_name, cfg, spp=None):
                       + (f", cgroup CPU quota {quota:g}" if quota else "") + f"), {dt:.2f} s wall"}
 
 
+def plan_launch(gpus, env, device_count):
+    """How `bench.py --gpus N` runs (decided before any GPU call):
+    ("run", world)  — this process is one rank of `world` (torchrun set WORLD_SIZE = N, or N = 1);
+    ("spawn", N)    — no launcher and N > 1: start N ranks with torch.distributed.run as a child
+                      process on this node and exit with its status;
+    ("error", msg)  — N disagrees with WORLD_SIZE, or the node has fewer than N GPUs.
+    It never renders N > 1 on one GPU.  device_count: torch.cuda.device_count() (counting does
+    not initialise the GPU on this image)."""
+    if gpus < 1:
+        return ("error", f"--gpus must be >= 1, got {gpus}")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        try:
+            world = int(ws)
+        except ValueError:
+            return ("error", f"WORLD_SIZE={ws!r} is not an integer")
+        if world != gpus:
+            return ("error", f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+        local = int(env.get("LOCAL_RANK", "0"))
+        if local >= device_count:
+            return ("error", f"LOCAL_RANK {local} but only {device_count} GPU(s) visible")
+        return ("run", world)
+    if gpus > device_count:
+        return ("error", f"--gpus {gpus} but only {device_count} GPU(s) visible")
+    return ("run", 1) if gpus == 1 else ("spawn", gpus)
+
+
+def spawn_ranks(n, argv):
+    """One rank per GPU via torch.distributed.run (child process; this process never touched
+    the GPU).  Returns the launcher's exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def hip_kernel_name(kid, sched, scene):
     """The HIP kernel behind an xrt_stats kernel family for this schedule / scene (the name
     rocprofv3 reports, which the PMC summaries are keyed by)."""
@@ -131,10 +175,17 @@ def main():
     import numpy as np
     import torch
 
+    action, what = plan_launch(args.gpus, os.environ, torch.cuda.device_count())
+    if action == "error":
+        print(f"bench.py: {what}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if action == "spawn":
+        sys.exit(spawn_ranks(what, sys.argv[1:]))
+
     from xraytracer_amd import abi, distributed, scenes
     from xraytracer_amd.renderer import HipRenderer
 
-    world = env_int("WORLD_SIZE", 1)
+    world = what
     rank = env_int("RANK", 0)
     local = env_int("LOCAL_RANK", 0)
     dist = None
@@ -173,8 +224,10 @@ def main():
     agg = {k: 0.0 for k in ("segments", "shadow_rays", "draws", "samples", "iterations", "rejected")}
     kms = np.zeros(abi.XRT_K_COUNT)
     kl = np.zeros(abi.XRT_K_COUNT)
+    reduce_s = 0.0
     for _ in range(args.steps):
         st = step(True)
+        reduce_s += sharded.last_reduce_s
         for k in agg:
             agg[k] += getattr(st, k)
         kms += np.array(list(st.kernel_ms))
@@ -187,6 +240,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist is not None:
         elapsed = distributed.max_over_ranks(elapsed, dist, device=dev)
+        reduce_s = distributed.max_over_ranks(reduce_s, dist, device=dev)
         agg = distributed.sum_counters(agg, dist, device=dev)
 
     if rank == 0:
@@ -286,6 +340,9 @@ def main():
             "roofline": roof,
             "cpu_baseline": None,
         }
+        if world > 1:   # the RCCL framebuffer reduce, inside ms_per_step (slowest rank)
+            out["config"]["reduce_ms_per_step"] = round(reduce_s / args.steps * 1e3, 3)
+            out["config"]["reduce_bytes"] = W * H * 3 * 4
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(args.config, cfg, args.cpu_spp)
         print(json.dumps(out), flush=True)

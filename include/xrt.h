@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 9
+#define XRT_ABI_VERSION 10
 
 /* ---- status codes ---------------------------------------------------------------- */
 enum {
@@ -181,14 +181,17 @@ typedef struct {
     uint64_t path_slots;         /* slots in flight (pixels of this shard)                 */
     uint64_t schedule;           /* XRT_SCHED_* the render ran                             */
     uint64_t stalled;            /* paths stopped by the VPT no-progress guard             */
-    /* launch geometry the render ran with (merged schedule; 0 otherwise) */
-    uint32_t slots_per_wave;     /* path slots per wave                                    */
+    /* launch geometry the render ran with (merged schedules; 0 otherwise) */
+    uint32_t slots_per_wave;     /* path slots per wave of the first step launch            */
     uint32_t group_lanes;        /* lanes sharing one slot's traces (1 = pair passes)      */
     uint32_t partitions;         /* live-list partitions                                   */
     uint32_t visits_per_launch;  /* path segments per slot per step launch                 */
     uint64_t rng_twists;         /* mt19937 blocks generated (624 words each) over all slots,
                                     including each slot's first: rng_twists - path_slots is
                                     the number of ring refills done while paths were live  */
+    uint64_t layout_launches[5]; /* merged schedules: step launches per slots-per-wave layout
+                                    64, 32, 16, 8, 4 (the layout is re-chosen every launch
+                                    from the live count)                                   */
 } xrt_stats;
 
 /* ---- context ----------------------------------------------------------------------- */

@@ -6,8 +6,11 @@ samples run in order on one RNG stream, so the first k samples of the full-spp r
 exactly a k-spp render: the bench's launch geometry (slots per wave, group traces,
 live-list partitions, segments per launch) depends only on the image size and the scene,
 which are the workload's own.  Each test asserts that geometry, then compares the image
-bit for bit and the path counters exactly.
+bit for bit (C3 and C4, whose oracle is the reference's linear scan over 1,001 spheres or
+51,236 triangles, on a subset of the GPU frame's rows) and the path counters exactly.
+C4 is also rendered as the row shard one rank of its 8-GPU configuration renders.
 """
+import functools
 import numpy as np
 import pytest
 
@@ -150,6 +153,76 @@ def test_c4_mesh_geometry(renderer, deep):
     ref, st = pyoracle.render(s, 160, 90, 2)
     compare(img, ref)
     counters_equal(g, st)
+
+
+# rows y % 64 == 3 of C4 at 2 spp: a subset of the full frame and of the row shard 3 of 8
+C4_SUB = (3, 64)
+
+
+@functools.lru_cache(maxsize=1)
+def c4_reference():
+    c = scenes.CONFIGS["C4"]
+    k, n = C4_SUB
+    return pyoracle.render(scenes.build("C4"), c["width"], c["height"], 2, shard_index=k, shard_count=n)
+
+
+def render_c4(renderer, **kw):
+    import torch
+
+    c = scenes.CONFIGS["C4"]
+    w, h = c["width"], c["height"]
+    scene = scenes.build("C4")
+    assert scene.desc.n_tris == 51200 + 36
+    renderer.spp = 2
+    renderer.upload(scene)
+    fb = torch.full((h, w, 3), 7.0, dtype=torch.float32, device="cuda:0")
+    renderer.render_device(scene, w, h, fb.data_ptr(), after_stream=torch.cuda.current_stream().cuda_stream,
+                           timing=True, schedule="auto", **kw)
+    return fb.cpu().numpy(), renderer.stats
+
+
+def test_c4_full_geometry(renderer):
+    """C4 at its own 1920x1080 through the bench's entry point (auto schedule,
+    device output): 1,024 live-list partitions, the BVH walk running; rows y % 64 == 3 bit-exact
+    against the oracle (Src/renderer.cpp:29-81, Src/primitive.cpp:83-168)."""
+    img, g = render_c4(renderer)
+    assert g.partitions == partitions(1920 * 1080) == 1024
+    assert g.samples == 1920 * 1080 * 2
+    if g.schedule == abi.XRT_SCHED_WAVEFRONT:
+        assert g.launches[abi.XRT_K_DEEP] > 0
+    ref, _ = c4_reference()
+    k, n = C4_SUB
+    compare(img[k::n], ref[k::n])
+
+
+def test_c4_row_shard(renderer):
+    """C4's multi-GPU configuration: the row shard rank 3 of 8 renders (rows y % 8 == 3, 135 x
+    1920 slots, 504 partitions); zeros elsewhere, and rows y % 64 == 3 (inside the shard)
+    bit-exact against the oracle."""
+    img, g = render_c4(renderer, shard_index=3, shard_count=8)
+    assert g.samples == 135 * 1920 * 2 and g.path_slots == 135 * 1920
+    assert g.partitions == partitions(135 * 1920) == 504
+    owned = np.zeros(1080, bool)
+    owned[3::8] = True
+    assert np.all(img[~owned] == 0)
+    ref, _ = c4_reference()
+    k, n = C4_SUB
+    compare(img[k::n], ref[k::n])
+
+
+def test_c5_full_frame(renderer):
+    """C5 (smoke VPT(10) on the 128^3 grid) at its own 800x600 through the
+    bench's entry point, 8 spp: 936 partitions, walks carried across several k_step launches
+    with refills, full frame bit-exact and counters equal (Src/integrator.h:409-473,
+    Src/medium.cpp:45-133)."""
+    img, ref, st, g = render_like_bench(renderer, "C5", 8)
+    assert g.schedule == abi.XRT_SCHED_STEP
+    assert g.partitions == partitions(800 * 600) == 936
+    assert g.launches[abi.XRT_K_STEP] >= 2, list(g.launches)
+    assert g.rng_twists > g.path_slots
+    compare(img, ref)
+    counters_equal(g, st)
+    assert st["segments"] > 0
 
 
 def test_c5_grid_geometry(renderer):

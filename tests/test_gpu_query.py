@@ -114,3 +114,36 @@ def test_cpp_host_query_api(tmp_path):
         assert np.array_equal(got[p:p + 7], np.concatenate([o, dd, [1.0]]).astype(np.float32)), k
         p += 7
     assert np.all(got[p:p + 128].reshape(-1, 2) == [1.0, 1.0])
+
+
+def test_occluded_query_lightless_two_level():
+    """an occluded query on a two-level scene (a big mesh among small
+    objects) with no area light queues every deep ray as a shadow ray of light 0; the deep
+    queues must hold them (part_cap per light of the trace kernel, at least one).  More rays
+    than several partitions' worth, bit-exact hit flags against the oracle."""
+    from xraytracer_amd import scenes as S
+    s = S.SceneBundle()
+    s.load_obj(S.CORNELL_OBJ)
+    s.add_sphere_mesh("sphere_mesh", (150.0, 420.0, 400.0), 90.0, 40, 40, (0.58, 0.58, 0.58))
+    s.flatten()
+    s.camera = S.pinhole(S.CORNELL_C2W, 60.0, 32, 18)
+    assert s.desc.n_lights == 0
+    rng = np.random.default_rng(11)
+    n = 20000
+    o = rng.uniform((60.0, 330.0, 310.0), (240.0, 510.0, 490.0), (n, 3))   # around the sphere mesh
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.concatenate([o, d], axis=1).astype(np.float32)
+    tmax = rng.uniform(0.0, 600.0, n).astype(np.float32)
+    r = HipRenderer(1, device=0)
+    got = r.query(s, rays, tmax=tmax, occluded=True)
+    ref = pyoracle.query(s, rays, tmax=tmax, occluded=True)
+    hits = [h.hit for h in ref]
+    assert [h.hit for h in got] == hits
+    assert 1000 < sum(hits) < n - 1000
+    # and the closest-hit query of the same rays
+    got = r.query(s, rays)
+    ref = pyoracle.query(s, rays)
+    for k in range(0, n, 7):
+        assert np.array_equal(record(got[k]), record(ref[k])), k
+    r.close()

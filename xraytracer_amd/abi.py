@@ -17,7 +17,7 @@ if os.environ.get("XRT_LIB"):   # experiment builds (csrc/Makefile `variant` -> 
     _v = os.path.join(HERE, "variants", os.environ["XRT_LIB"])
     LIB_PATH = _v if os.path.exists(_v) else os.path.join(HERE, os.environ["XRT_LIB"])
 
-XRT_ABI_VERSION = 9   # include/xrt.h XRT_ABI_VERSION
+XRT_ABI_VERSION = 10  # include/xrt.h XRT_ABI_VERSION
 XRT_OK = 0
 XRT_OBJ_MESH, XRT_OBJ_SPHERE, XRT_OBJ_BOX = 0, 1, 2
 XRT_LIGHT_QUAD, XRT_LIGHT_TRIANGLE, XRT_LIGHT_SPHERE = 0, 1, 2
@@ -31,6 +31,7 @@ XRT_SCHED_WAVEFRONT, XRT_SCHED_STEP, XRT_SCHED_STEP_TRI, XRT_SCHED_STEP_MERGED =
 SCHEDULE_NAMES = ("wavefront", "step", "step_tri", "step_merged")
 XRT_K_SEED, XRT_K_TRACE, XRT_K_SHADE, XRT_K_FINISH, XRT_K_STEP, XRT_K_REFILL, XRT_K_DEEP, XRT_K_COUNT = \
     0, 1, 2, 3, 4, 5, 6, 7
+LAYOUTS = (64, 32, 16, 8, 4)   # xrt_stats.layout_launches: slots per wave
 KERNEL_NAMES = ("seed", "trace", "shade", "finish", "step", "refill", "trace_deep4")
 
 INTEGRATORS = {"gi": XRT_INTEGRATOR_GI, "direct": XRT_INTEGRATOR_DIRECT, "vpt": XRT_INTEGRATOR_VPT,
@@ -91,10 +92,11 @@ class XrtStats(C.Structure):
                 ("rejected", C.c_uint64), ("iterations", C.c_uint64), ("path_slots", C.c_uint64),
                 ("schedule", C.c_uint64), ("stalled", C.c_uint64), ("slots_per_wave", C.c_uint32),
                 ("group_lanes", C.c_uint32), ("partitions", C.c_uint32), ("visits_per_launch", C.c_uint32),
-                ("rng_twists", C.c_uint64)]
+                ("rng_twists", C.c_uint64), ("layout_launches", C.c_uint64 * 5)]
 
     def as_dict(self):
-        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "launches")}
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "launches", "layout_launches")}
+        d["layout_launches"] = dict(zip(LAYOUTS, (int(x) for x in self.layout_launches)))
         d["kernel_ms"] = {n: self.kernel_ms[i] for i, n in enumerate(KERNEL_NAMES)}
         d["launches"] = {n: int(self.launches[i]) for i, n in enumerate(KERNEL_NAMES)}
         return d

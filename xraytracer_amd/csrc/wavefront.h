@@ -144,8 +144,6 @@ struct StepObjs {
 constexpr uint32_t kBvhLeaf = 4;      // BVH: primitives per leaf (at most)
 constexpr int kBvhMaxDepth = 48;      // BVH build: depth bound (SAH above max - 24 levels, median below)
 constexpr int kBvhStack = 24;         // k_trace_bvh: LDS traversal stack entries per thread (> tree depth)
-constexpr uint32_t kDeepQuadSlots = 0xffffffffu;   // path slots below which k_trace_deep4q runs: every size since
-                                                   // its lanes keep their own best hits
 constexpr int kBvh4Stack = 48;        // k_trace_deep4: LDS stack entries per lane (>= 3 * 4-wide depth + 1)
 constexpr int kSphBvhMin = 16;        // sphere scenes with at least this many spheres get a skip-link BVH
 constexpr int kSmallTris = 1024;   // scenes up to this size keep every triangle in LDS

@@ -120,12 +120,14 @@ T* as(DevBuf& b) {
 
 uint32_t shard_rows(uint32_t h, uint32_t idx, uint32_t n) { return idx < h ? (h - idx + n - 1) / n : 0; }
 
-// two-level trace queues (KParams::deep): per partition part_cap * (1 + lights) entries, then
-// kMaxParts counts and kMaxParts fetch counters (k_trace_deep_pt)
+// two-level trace queues (KParams::deep): per partition part_cap extension-ray entries, then
+// the shadow rays from entry part_cap on — part_cap per light of the trace kernel, which is
+// instantiated for at least one light (an occluded query on a light-less scene queues its
+// rays as shadow rays of light 0) — then kMaxParts counts, fetch counters and shadow counts
 int setup_deep(xrt_ctx* c, KParams& P) {
     P.deep = nullptr, P.deep_count = nullptr, P.deep_cap = 0;
     if (!P.two_level) return XRT_OK;
-    P.deep_cap = P.part_cap * (1u + (uint32_t)P.n_lights);
+    P.deep_cap = P.part_cap * (1u + (uint32_t)std::max(1, P.n_lights));
     const size_t words = (size_t)P.n_part * P.deep_cap + 3 * kMaxParts;   // queues, counts, fetch counters
     const int rc = ensure(c, c->deep, words * 4);
     if (rc) return rc;
@@ -621,24 +623,37 @@ static int set_medium_one(xrt_ctx* c, const xrt_medium_desc* m) {
 #ifndef XRT_CORNER_GRID
 #define XRT_CORNER_GRID 1
 #endif
-    // the per-cell corner layout (8x the grid's bytes; skipped above 2 GiB)
+    // the per-cell corner layout (8x the grid's bytes; skipped above 2 GiB).  It is only an
+    // acceleration: when the host copy or the device buffer cannot be had, the medium reads
+    // the dense grid's rows instead (D.corners = null), with identical results.
     const size_t cx = m->nx - 1, cy = m->ny - 1, cz = m->nz - 1, cells = cx * cy * cz;
+    free_buf(c->corners);
     if (XRT_CORNER_GRID && cells && cells * 32 <= (size_t(2) << 30)) {
-        std::vector<float> cor(cells * 8);
-        const float* g = m->density;
-        const size_t sy = m->nx, sz = (size_t)m->nx * m->ny;
-        for (size_t k = 0; k < cz; ++k)
-            for (size_t j = 0; j < cy; ++j)
-                for (size_t i = 0; i < cx; ++i) {
-                    const float* b = g + k * sz + j * sy + i;
-                    float* o = cor.data() + 8 * ((k * cy + j) * cx + i);
-                    o[0] = b[0], o[1] = b[sz], o[2] = b[sy], o[3] = b[sy + sz];
-                    o[4] = b[1], o[5] = b[1 + sz], o[6] = b[1 + sy], o[7] = b[1 + sy + sz];
-                }
-        if ((rc = upload(c, c->corners, cor.data(), cor.size() * sizeof(float)))) return rc;
-        D.corners = as<float>(c->corners);
-    } else {
-        free_buf(c->corners);
+        std::vector<float> cor;
+        try {
+            cor.resize(cells * 8);
+        } catch (const std::bad_alloc&) {
+            cor.clear();
+        }
+        if (!cor.empty()) {
+            const float* g = m->density;
+            const size_t sy = m->nx, sz = (size_t)m->nx * m->ny;
+            for (size_t k = 0; k < cz; ++k)
+                for (size_t j = 0; j < cy; ++j)
+                    for (size_t i = 0; i < cx; ++i) {
+                        const float* b = g + k * sz + j * sy + i;
+                        float* o = cor.data() + 8 * ((k * cy + j) * cx + i);
+                        o[0] = b[0], o[1] = b[sz], o[2] = b[sy], o[3] = b[sy + sz];
+                        o[4] = b[1], o[5] = b[1 + sz], o[6] = b[1 + sy], o[7] = b[1 + sy + sz];
+                    }
+            if (upload(c, c->corners, cor.data(), cor.size() * sizeof(float)) == XRT_OK) {
+                D.corners = as<float>(c->corners);
+            } else {
+                free_buf(c->corners);
+                (void)hipGetLastError();
+                c->err.clear();
+            }
+        }
     }
     return set_medium_grid(c, m);
 }
@@ -781,23 +796,26 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     P.cdiv = (cdiv_exact(c, P.fw) ? 1u : 0u) | (cdiv_exact(c, P.fh) ? 2u : 0u) | (cdiv_exact(c, P.aspect) ? 4u : 0u);
     P.shard_index = p->shard_index, P.shard_count = p->shard_count, P.n_slots = (uint32_t)n;
     P.spw_req = p->slots_per_wave, P.rflags = p->flags;
-    // two-level traces: four lanes per queued ray below kDeepQuadSlots path slots (the deep
-    // walk's launch is then bound by its longest walk, not by its total work)
+    // two-level traces: the BVH walk takes four lanes per queued ray (k_trace_deep4q, every
+    // size: its lanes keep their own best hits) unless the caller asks for one
     {
         const char* dq = exp_env("XRT_DEEP_QUAD");
-        P.deep_quad = dq                                  ? std::atoi(dq)
-                      : (p->flags & XRT_FLAG_DEEP_SINGLE) ? 0
-                      : (p->flags & XRT_FLAG_DEEP_QUAD)   ? 1
-                                                          : (n < kDeepQuadSlots ? 1 : 0);
+        P.deep_quad = dq ? std::atoi(dq) : (p->flags & XRT_FLAG_DEEP_SINGLE) ? 0 : 1;
     }
+    // Schedule, decided once (the partition count below depends on it): the fused k_step
+    // (scene resident in LDS, kStepVisits path segments per slot per launch, in-kernel
+    // compaction and refill requests) when the scene fits, in its merged-trace form for small
+    // triangle scenes; else the multi-pass wavefront (k_shade, then k_trace streaming the
+    // scene through LDS tiles; k_shade refills its slots' rings in-line).
+    const bool fused = !(p->flags & XRT_FLAG_WAVEFRONT) && step_lds_bytes(P) != 0;
+    const bool merged = fused && !(p->flags & XRT_FLAG_NO_MERGED) && use_step_merged(P);
     // live-list partitions (a multiple of the 8 XCDs): every wave appends to its partition's
     // counters once per launch, so more partitions mean less atomic contention (64 -> 256:
     // C4 -14%, C2 -4.5%).  The merged schedule (64 segments per launch) is fastest with
     // >= 2048 slots per partition (at most 256), the per-segment ones with >= 512 (at most
     // kMaxParts): C3 -8%, C4 -4% over 256
     {
-        const bool merged_sched = !(p->flags & XRT_FLAG_WAVEFRONT) && step_lds_bytes(P) != 0 &&
-                                  !(p->flags & XRT_FLAG_NO_MERGED) && use_step_merged(P);
+        const bool merged_sched = merged;
         const size_t cap = merged_sched ? 256 : kMaxParts, per = merged_sched ? 2048 : kPartMinSlots;
         uint32_t np = (uint32_t)std::min<size_t>(cap, std::max<size_t>(1, n / per));
         if (np >= 8) np &= ~7u;
@@ -887,14 +905,9 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     uint64_t it = 0;
     int poll_slot = 0;
     bool done = false;
-    // Schedule: the fused k_step (scene resident in LDS, kStepVisits path segments per
-    // slot per launch, in-kernel compaction and refill requests; k_refill every
-    // kStepRefill rounds) when the scene fits, else the multi-pass wavefront (k_shade, then
-    // k_trace streaming the scene through LDS tiles; k_shade refills its slots' rings
-    // in-line).  k_step rotates three live counters: round i reads counts[i%3], appends
-    // to counts[(i+1)%3] and clears counts[(i+2)%3] for round i+1.
-    const bool fused = !(p->flags & XRT_FLAG_WAVEFRONT) && step_lds_bytes(P) != 0;
-    const bool merged = fused && !(p->flags & XRT_FLAG_NO_MERGED) && use_step_merged(P);
+    // k_step rotates three live counters: round i reads counts[i%3], appends to
+    // counts[(i+1)%3] and clears counts[(i+2)%3] for round i+1 (k_refill every kStepRefill
+    // rounds unless the kernel refills in-line).
     // segments per slot per step launch: kMergedVisits / kStepVisits unless the caller
     // sets visits_per_launch (results do not depend on it)
     const uint32_t merged_visits =
@@ -941,6 +954,10 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             const int ci = (int)(it % 3), co = (int)((it + 1) % 3), cz = (int)((it + 2) % 3);
             live = counts_at(co);
             launch_live.push_back(live_hint);
+            if (merged) {
+                const uint32_t spw = step_merged_spw(P, live_hint);
+                S.layout_launches[spw == 64 ? 0 : spw == 32 ? 1 : spw == 16 ? 2 : spw == 8 ? 3 : 4]++;
+            }
             hipError_t e = launch(XRT_K_STEP, [&] {
                 if (merged)
                     return launch_step_merged(P, dP, c->step_objs, lists[cur], counts_at(ci), lists[nxt],
@@ -1032,7 +1049,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     S.partitions = P.n_part;
     if (fused) S.visits_per_launch = step_visits;
     if (merged) {
-        S.slots_per_wave = step_merged_spw(P, n);   // the layout of the first launch
+        S.slots_per_wave = step_merged_spw(P, n);   // the layout of the first launch (every launch's: layout_launches)
         S.group_lanes = step_merged_group(P, S.slots_per_wave);
     }
     if (timing) {
@@ -1203,6 +1220,7 @@ static int render_multi(xrt_ctx* m, const xrt_render_params* p, float* d_out, fl
             T.samples += S[i].samples, T.segments += S[i].segments, T.shadow_rays += S[i].shadow_rays;
             T.draws += S[i].draws, T.rejected += S[i].rejected, T.stalled += S[i].stalled;
             T.rng_twists += S[i].rng_twists;
+            for (int k = 0; k < 5; ++k) T.layout_launches[k] += S[i].layout_launches[k];
             T.path_slots += S[i].path_slots;
             T.iterations = std::max(T.iterations, S[i].iterations);
         }

@@ -83,6 +83,7 @@ class ShardedRenderer:
         self.dist = dist
         self.dst = dst
         self.rank, self.world = _world(dist)
+        self.last_reduce_s = 0.0   # host time of the last render()'s framebuffer reduce
         if not 0 <= dst < self.world:
             raise ValueError(f"dst rank {dst} outside world of {self.world}")
 
@@ -100,5 +101,12 @@ class ShardedRenderer:
             after_stream = torch.cuda.current_stream(fb.device).cuda_stream
         st = self.renderer.render_device(scene, width, height, fb.data_ptr(), shard_index=self.rank,
                                          shard_count=self.world, after_stream=after_stream, **kw)
+        # the render has returned with the image complete; the reduce is timed on its own
+        # (host clock to its completion: the next render would wait for it anyway)
+        import time
+        t0 = time.perf_counter()
         reduce_framebuffer(fb, self.dist, self.dst)
+        if self.world > 1 and fb.is_cuda:
+            torch.cuda.synchronize(fb.device)
+        self.last_reduce_s = time.perf_counter() - t0
         return st
