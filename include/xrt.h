@@ -164,9 +164,13 @@ enum {
 };
 
 /* device schedules: multi-pass wavefront (k_shade + k_trace), fused per-slot k_step with
- * the scene in LDS, its triangle-scene form with cooperative (ray, triangle) traces, and
- * that form with one merged trace (shadow rays + next extension ray) per segment */
-enum { XRT_SCHED_WAVEFRONT = 0, XRT_SCHED_STEP = 1, XRT_SCHED_STEP_TRI = 2, XRT_SCHED_STEP_MERGED = 3 };
+ * the scene in LDS, its triangle-scene form with cooperative (ray, triangle) traces, that
+ * form with one merged trace (shadow rays + next extension ray) per segment, and the merged
+ * form for two-level scenes (small objects in LDS, a big mesh's BVH walked by the wave) */
+enum {
+    XRT_SCHED_WAVEFRONT = 0, XRT_SCHED_STEP = 1, XRT_SCHED_STEP_TRI = 2, XRT_SCHED_STEP_MERGED = 3,
+    XRT_SCHED_STEP_BVH = 4
+};
 
 typedef struct {
     double wall_ms;              /* host wall clock of the render call (upload excluded) */

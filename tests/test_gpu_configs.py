@@ -136,20 +136,26 @@ def test_c3_geometry(renderer):
     counters_equal(g, st)
 
 
-@pytest.mark.parametrize("deep", ["auto", "single", "quad"])
-def test_c4_mesh_geometry(renderer, deep):
+@pytest.mark.parametrize("sched,deep", [("auto", "auto"), ("wavefront", "auto"), ("wavefront", "single"),
+                                        ("wavefront", "quad")])
+def test_c4_mesh_geometry(renderer, sched, deep):
     """C4's own mesh: SphereMesh(nTheta = nPhi = 160) = 51,200 triangles + the Cornell box
-    (51,236), at C4's 16:9 aspect (160x90): wavefront schedule with the two-level trace, the
-    BVH walked with four lanes per queued ray (the default, what the bench runs) and with
+    (51,236), at C4's 16:9 aspect (160x90): the fused two-level schedule (merged kernel, the
+    small objects by pair passes, the BVH walked by the wave's quads — what the bench runs)
+    and the wavefront schedule with the BVH walked with four lanes per queued ray and with
     one (XRT_FLAG_DEEP_SINGLE)."""
     s = scenes.cornell_spheremesh(160, 90)
     assert s.desc.n_tris == 51200 + 36
     renderer.spp = 2
     renderer.upload(s)
-    img = renderer.render(s, 160, 90, timing=True, deep=deep)
+    img = renderer.render(s, 160, 90, timing=True, deep=deep, schedule=sched)
     g = renderer.stats
-    assert g.schedule == abi.XRT_SCHED_WAVEFRONT and g.launches[abi.XRT_K_STEP] == 0
-    assert g.launches[abi.XRT_K_DEEP] == g.launches[abi.XRT_K_TRACE] > 0
+    if sched == "auto":
+        assert g.schedule == abi.XRT_SCHED_STEP_BVH and g.launches[abi.XRT_K_STEP] > 0
+        assert g.launches[abi.XRT_K_TRACE] == g.launches[abi.XRT_K_DEEP] == g.launches[abi.XRT_K_SHADE] == 0
+    else:
+        assert g.schedule == abi.XRT_SCHED_WAVEFRONT and g.launches[abi.XRT_K_STEP] == 0
+        assert g.launches[abi.XRT_K_DEEP] == g.launches[abi.XRT_K_TRACE] > 0
     ref, st = pyoracle.render(s, 160, 90, 2)
     compare(img, ref)
     counters_equal(g, st)
@@ -183,13 +189,14 @@ def render_c4(renderer, **kw):
 
 def test_c4_full_geometry(renderer):
     """C4 at its own 1920x1080 through the bench's entry point (auto schedule,
-    device output): 1,024 live-list partitions, the BVH walk running; rows y % 64 == 3 bit-exact
-    against the oracle (Src/renderer.cpp:29-81, Src/primitive.cpp:83-168)."""
+    device output): the fused two-level kernel over 256 live-list partitions across several
+    launches; rows y % 64 == 3 bit-exact against the oracle (Src/renderer.cpp:29-81,
+    Src/primitive.cpp:83-168)."""
     img, g = render_c4(renderer)
-    assert g.partitions == partitions(1920 * 1080) == 1024
+    assert g.schedule == abi.XRT_SCHED_STEP_BVH
+    assert g.partitions == partitions(1920 * 1080, merged=True) == 256
     assert g.samples == 1920 * 1080 * 2
-    if g.schedule == abi.XRT_SCHED_WAVEFRONT:
-        assert g.launches[abi.XRT_K_DEEP] > 0
+    assert g.launches[abi.XRT_K_STEP] >= 2 and g.layout_launches[0] >= 1   # full waves first
     ref, _ = c4_reference()
     k, n = C4_SUB
     compare(img[k::n], ref[k::n])
@@ -197,11 +204,12 @@ def test_c4_full_geometry(renderer):
 
 def test_c4_row_shard(renderer):
     """C4's multi-GPU configuration: the row shard rank 3 of 8 renders (rows y % 8 == 3, 135 x
-    1920 slots, 504 partitions); zeros elsewhere, and rows y % 64 == 3 (inside the shard)
+    1920 slots, 120 partitions); zeros elsewhere, and rows y % 64 == 3 (inside the shard)
     bit-exact against the oracle."""
     img, g = render_c4(renderer, shard_index=3, shard_count=8)
+    assert g.schedule == abi.XRT_SCHED_STEP_BVH
     assert g.samples == 135 * 1920 * 2 and g.path_slots == 135 * 1920
-    assert g.partitions == partitions(135 * 1920) == 504
+    assert g.partitions == partitions(135 * 1920, merged=True) == 120
     owned = np.zeros(1080, bool)
     owned[3::8] = True
     assert np.all(img[~owned] == 0)

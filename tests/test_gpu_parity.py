@@ -356,19 +356,51 @@ def test_normal_integrator_on_medium_box(renderer, sched):
     compare(img, ref)
 
 
-@pytest.mark.parametrize("deep", ["single", "quad"])
+@pytest.mark.parametrize("deep", ["fused", "single", "quad"])
 @pytest.mark.parametrize("nt,w,h,spp", [(24, 64, 36, 4), (80, 48, 30, 3), (380, 12, 9, 2)])
 def test_c4_sphere_mesh_gi(renderer, nt, w, h, spp, deep):
     """Config C4 scene family (Cornell + tessellated sphere; 1,152, 12,800 and 288,800 mesh
-    triangles) at reduced size: the wavefront schedule with BVH traces, bit-exact against
-    the oracle's linear scan, counters included.  The largest tree has more than 65,536
-    nodes, so its traversal stack takes 32-bit entries (16-bit for the others)."""
+    triangles) at reduced size, bit-exact against the oracle's linear scan, counters
+    included: the fused two-level schedule (merged kernel + the wave's quad BVH walk) and
+    the wavefront schedule with one or four lanes per deep ray.  The largest binary tree has
+    more than 65,536 nodes, so the wavefront traversal stack takes 32-bit entries."""
     s = scenes.cornell_spheremesh(w, h, n_theta=nt, n_phi=nt)
-    img, ref, st = render_both(renderer, s, w, h, spp, deep=deep)
+    if deep == "fused":
+        img, ref, st = render_both(renderer, s, w, h, spp, schedule="auto")
+    else:
+        img, ref, st = render_both(renderer, s, w, h, spp, deep=deep, schedule="wavefront")
     compare(img, ref)
     g = renderer.stats
-    assert g.launches[abi.XRT_K_STEP] == 0   # too large for LDS: multi-pass schedule
-    assert g.schedule == abi.XRT_SCHED_WAVEFRONT
+    if deep == "fused":
+        assert g.schedule == abi.XRT_SCHED_STEP_BVH and g.launches[abi.XRT_K_DEEP] == 0
+    else:
+        assert g.launches[abi.XRT_K_STEP] == 0   # multi-pass schedule
+        assert g.schedule == abi.XRT_SCHED_WAVEFRONT
+    assert (g.segments, g.shadow_rays, g.draws) == (st["segments"], st["shadow_rays"], st["draws"])
+
+
+@pytest.mark.parametrize("integ", ["gi", "direct"])
+@pytest.mark.parametrize("spw", [0, 16, 32, 64])
+def test_two_level_fused_layouts_and_lights(renderer, integ, spw):
+    """The fused two-level kernel (k_step_merged<..., BVH>) with two area lights (a quad and a
+    triangle light: NL = 2), GI and Direct, at every slots-per-wave layout, and a few visits
+    per launch so paths and their RNG windows cross launches: bit-exact with counters equal."""
+    s = scenes.SceneBundle()
+    s.load_obj(scenes.CORNELL_OBJ)
+    s.add_quad_light("QuadLight", (343.0, 548.0, 227.0), (343.0, 548.0, 332.0), (213.0, 548.0, 227.0),
+                     (25.0, 25.0, 25.0))
+    s.add_triangle_light("TriLight", (100.0, 500.0, 100.0), (150.0, 500.0, 100.0), (100.0, 500.0, 150.0),
+                         (10.0, 5.0, 2.0))
+    s.add_sphere_mesh("sphere_mesh", (150.0, 420.0, 400.0), 90.0, 60, 60, (0.58, 0.58, 0.58))
+    s.flatten()
+    s.camera = scenes.pinhole(scenes.CORNELL_C2W, 60.0, 72, 40)
+    img, ref, st = render_both(renderer, s, 72, 40, 5, integrator=integ, schedule="auto", slots_per_wave=spw,
+                               visits_per_launch=3)
+    compare(img, ref)
+    g = renderer.stats
+    assert g.schedule == abi.XRT_SCHED_STEP_BVH and g.launches[abi.XRT_K_STEP] > 2
+    if spw:
+        assert g.layout_launches[abi.LAYOUTS.index(spw)] == g.launches[abi.XRT_K_STEP]
     assert (g.segments, g.shadow_rays, g.draws) == (st["segments"], st["shadow_rays"], st["draws"])
 
 

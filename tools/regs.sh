@@ -1,8 +1,9 @@
 #!/bin/bash
-# tools/regs.sh [pattern] — per-kernel VGPR/SGPR/spill/occupancy of wavefront.hip (gfx950)
+# tools/regs.sh [pattern] — per-kernel VGPR/SGPR/spill/occupancy of $SRC (default wavefront.hip;
+# SRC=step_tri.hip for the merged kernels), gfx950; extra -D flags in $REGS_DEFS
 cd "$(dirname "$0")/../xraytracer_amd/csrc"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -I../../include -I. --offload-arch=gfx950 \
-    $REGS_DEFS -c wavefront.hip -o /tmp/regs_wf.o -Rpass-analysis=kernel-resource-usage 2>&1 |
+    $REGS_DEFS -c ${SRC:-wavefront.hip} -o /tmp/regs_wf.o -Rpass-analysis=kernel-resource-usage 2>&1 |
 python3 -c '
 import re, sys
 pat = sys.argv[1] if len(sys.argv) > 1 else ""

@@ -25,6 +25,7 @@ def main():
     spw = ([int(a.split("=")[1]) for a in sys.argv if a.startswith("--spw=")] or [0])[0]
     group = "--no-group" not in sys.argv
     deep = ([a.split("=")[1] for a in sys.argv if a.startswith("--deep=")] or ["auto"])[0]
+    sched = ([a.split("=")[1] for a in sys.argv if a.startswith("--schedule=")] or ["auto"])[0]
     cfg = scenes.CONFIGS[cfg_name]
     W, H, SPP = cfg["width"], cfg["height"], cfg["spp"]
     SPP = ([int(a.split("=")[1]) for a in sys.argv if a.startswith("--spp=")] or [SPP])[0]
@@ -42,14 +43,15 @@ def main():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             st = r.render_device(scene, W, H, fb.data_ptr(), shard_index=s, shard_count=n, timing=timing,
-                                 slots_per_wave=spw, group=group, deep=deep)
+                                 slots_per_wave=spw, group=group, deep=deep, schedule=sched)
             torch.cuda.synchronize()
             times.append(time.perf_counter() - t0)
         slow = max(times)
         res[n] = {"shard_ms": [round(t * 1e3, 2) for t in times],
                   "kernel_ms": {abi.KERNEL_NAMES[i]: round(st.kernel_ms[i], 2) for i in range(abi.XRT_K_COUNT)
                                 if st.kernel_ms[i]},
-                  "msamples_s": round(W * H * SPP / slow / 1e6, 1), "iterations": int(st.iterations)}
+                  "msamples_s": round(W * H * SPP / slow / 1e6, 1), "iterations": int(st.iterations),
+                  "schedule": abi.SCHEDULE_NAMES[st.schedule]}
         print(n, res[n], flush=True)
     print(json.dumps({"config": cfg_name, "shards": res}))
     r.close()

@@ -27,8 +27,8 @@ XRT_INTEGRATOR_INDIRECT, XRT_INTEGRATOR_NORMAL, XRT_INTEGRATOR_VPT_NEE = 3, 4, 5
 XRT_MEDIUM_HETEROGENEOUS, XRT_MEDIUM_HOMOGENEOUS_MIS, XRT_MEDIUM_HOMOGENEOUS_ACHROMATIC, XRT_MEDIUM_HOMOGENEOUS_NOMIS = 0, 1, 2, 3
 XRT_FLAG_TIMING, XRT_FLAG_WAVEFRONT, XRT_FLAG_NO_MERGED, XRT_FLAG_NO_GROUP, XRT_FLAG_ACCUMULATE = 1, 2, 4, 8, 16
 XRT_FLAG_DEEP_SINGLE, XRT_FLAG_DEEP_QUAD = 32, 64
-XRT_SCHED_WAVEFRONT, XRT_SCHED_STEP, XRT_SCHED_STEP_TRI, XRT_SCHED_STEP_MERGED = 0, 1, 2, 3
-SCHEDULE_NAMES = ("wavefront", "step", "step_tri", "step_merged")
+XRT_SCHED_WAVEFRONT, XRT_SCHED_STEP, XRT_SCHED_STEP_TRI, XRT_SCHED_STEP_MERGED, XRT_SCHED_STEP_BVH = 0, 1, 2, 3, 4
+SCHEDULE_NAMES = ("wavefront", "step", "step_tri", "step_merged", "step_bvh")
 XRT_K_SEED, XRT_K_TRACE, XRT_K_SHADE, XRT_K_FINISH, XRT_K_STEP, XRT_K_REFILL, XRT_K_DEEP, XRT_K_COUNT = \
     0, 1, 2, 3, 4, 5, 6, 7
 LAYOUTS = (64, 32, 16, 8, 4)   # xrt_stats.layout_launches: slots per wave

@@ -43,6 +43,7 @@ hipError_t launch_step(const KParams& P, const KParams* dP, const uint32_t* list
 // draw, LDS bytes, the per-object kernel-argument records, and the launch (same list /
 // counter contract as launch_step)
 bool use_step_merged(const KParams& P);
+bool use_step_bvh(const KParams& P);     // two-level scenes: the merged kernel with the wave's BVH walk
 uint32_t step_merged_draws(const KParams& P);
 uint32_t step_merged_spw(const KParams& P, uint64_t live);   // slots per wave for `live` live slots
 uint32_t step_merged_group(const KParams& P, uint32_t spw);  // lanes per slot in group traces (1 = none)

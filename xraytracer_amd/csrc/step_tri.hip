@@ -29,6 +29,7 @@
 //
 // GIIntegrator with maxDepth 0 and scenes with more than kMergedMaxObjs objects keep using
 // k_step_tri.
+#include "bvh.h"
 #include "launch.h"
 #include "path_common.h"
 
@@ -36,6 +37,13 @@ namespace xrt {
 
 using gu32 = __attribute__((address_space(1))) const uint32_t;
 using gf32 = __attribute__((address_space(1))) const float;
+// one float4 by a global (not flat) load
+__device__ __forceinline__ f4 ldg4(const f4* p, size_t i) {
+    typedef float fv4 __attribute__((ext_vector_type(4)));
+    using gv4 = __attribute__((address_space(1))) const fv4;
+    const fv4 v = ((gv4*)p)[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
 // global-address-space view of a generic pointer to device memory: global_load instead of
 // flat_load (a flat load also counts in lgkmcnt, so every LDS wait would wait for it too)
 template <class G, class T>
@@ -200,8 +208,10 @@ __device__ __forceinline__ bool ray_tri_nb(v3 o, v3 d, v3 v0, v3 e1, v3 e2, floa
 }
 
 // One cooperative trace of the wave: the extension ray (closest hit, if `ext`) and the
-// pending shadow rays (any hit, bits of `shm`).
-template <int NL>
+// pending shadow rays (any hit, bits of `shm`).  ORIG: the closest-hit key's low word is the
+// triangle's original index (the w of its third float4, KParams::stri) instead of its LDS
+// index — two-level scenes, whose BVH walk merges in the same (t, original index) order.
+template <int NL, bool ORIG = false>
 __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L, MergedWave<NL>& W, int lane,
                                              bool ext, v3 o, v3 d, uint32_t shm, const v3 (&so)[NL + 1],
                                              const v3 (&sd)[NL + 1], const float (&stm)[NL + 1],
@@ -258,11 +268,12 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
                 const f4 D = W.rd[r];
                 const uint32_t e = __float_as_uint(D.w);
                 float t;
-                const bool hit = ray_tri_nb(xyz(A), xyz(D), xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]),
-                                            xyz(L.tri[3 * k + 2]), t);
+                const f4 C = L.tri[3 * k + 2];
+                const bool hit = ray_tri_nb(xyz(A), xyz(D), xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(C), t);
                 if (hit) {
                     if (e < 64u)
-                        atomicMin(&W.best[e], ((unsigned long long)__float_as_uint(t) << 32) | k);
+                        atomicMin(&W.best[e], ((unsigned long long)__float_as_uint(t) << 32) |
+                                                  (ORIG ? __float_as_uint(C.w) : k));
                     else if (t < A.w)
                         atomicOr(&W.occ[e & 63u], 1u << ((e >> 6) - 1u));
                 }
@@ -357,6 +368,207 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const D
     }
     best = group_min64<G>(bk);
     occ = group_or32<G>(oc);
+}
+
+// ------------------------------------------- two-level trace inside the wave ----
+// The fused schedule for two-level scenes (C4: the Cornell box around a 51,200-triangle
+// sphere mesh; k_step_merged<..., BVH = true>): after merged_trace has tested the small
+// objects (LDS, pair passes, keys (t bits << 32 | original index)), the rays whose segment
+// still reaches the BVH — extension rays over [0, best t], shadow rays over [0, tmax] if no
+// small object occluded them — are ranked into the wave's scratch and walked by the wave's
+// 16 quads, k_trace_deep4q's four-lanes-per-ray walk of the 4-wide BVH (lane c owns child
+// c of the current node; the quad shares the pruning limit, occlusion and the next node by
+// DPP), a quad taking the next ranked ray when its walk ends.  Results merge into the
+// wave's records as merged_trace leaves them: the smallest (t, original index) key by the
+// lane holding it, occlusion bits by an or.  Exact for the reasons k_trace_deep4q is (every
+// triangle whose padded box overlaps [0, best t] is tested by some lane) — the same
+// lexicographic minimum over every triangle the reference's linear scan tests
+// (Src/scene.cpp:190-211, Src/primitive.cpp:83-168).
+
+// One leaf's triangles (BVH leaf order, KParams::bvh_tri: e1.w = occluder, e2.w = original
+// index) against a ray: closest hit as the (t, original index) minimum, or any occluder hit
+// below tmax.  The loads of the whole leaf are issued before the first test.  Mesh::
+// rayTriangleIntersect's decisions via ray_tri_nb (two-level scenes are det_bounded).
+#ifndef XRT_DEEP_LEAF_BATCH
+#define XRT_DEEP_LEAF_BATCH 4   // triangles whose loads are issued together (1, 2 or 4): registers vs latency
+#endif
+template <bool ANY>
+__device__ __forceinline__ bool deep_leaf(const KParams& P, int first, int count, v3 o, v3 d, float tmax, float& bt,
+                                          int& bk) {
+    constexpr int B = XRT_DEEP_LEAF_BATCH;
+    static_assert(kBvhLeaf % B == 0, "leaf batches");
+    bool occ = false;
+#pragma unroll
+    for (int q0 = 0; q0 < (int)kBvhLeaf; q0 += B) {
+        if (q0 >= count) break;
+        f4 T[B][3];
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+            if (q0 + q < count) {
+                const size_t i = 3 * (size_t)(first + q0 + q);
+                T[q][0] = ldg4(P.bvh_tri, i), T[q][1] = ldg4(P.bvh_tri, i + 1), T[q][2] = ldg4(P.bvh_tri, i + 2);
+            }
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+            if (q0 + q >= count) break;
+            if (ANY && T[q][1].w == 0.0f) continue;   // area-light objects never occlude
+            float t;
+            if (!ray_tri_nb(o, d, xyz(T[q][0]), xyz(T[q][1]), xyz(T[q][2]), t)) continue;
+            if (ANY) {
+                occ |= t < tmax;
+            } else {
+                const int k = __float_as_int(T[q][2].w);
+                if (t < bt || (t == bt && k < bk)) bt = t, bk = k;
+            }
+        }
+    }
+    return occ;
+}
+
+// The walk of n_deep ranked rays W.ro / W.rd (w: tmax resp. the ray id q * 64 + lane).
+// top: the first ntop 4-wide nodes in LDS; stk: this wave's 16 quad stacks (stride 16).
+// Must be called by every lane of the wave.
+template <int NL, typename SE>
+__device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, int ntop, SE* stk, MergedWave<NL>& W,
+                                               int lane, uint32_t n_deep) {
+    constexpr uint64_t kLeads = 0x1111111111111111ull;   // lane 0 of every quad
+    const int c = lane & 3;
+    SE* qs = stk + (lane >> 2);
+    uint32_t next = 0;   // wave-uniform: first ray not yet taken
+    bool active = false, any = false;
+    uint32_t id = 0;
+    int node = 0, sp = 0, bk = -1;
+    v3 o = mk(0, 0, 0), d = mk(0, 0, 0), inv = mk(0, 0, 0);
+    float tmax = 0.0f, bt = kINF;
+    while (true) {
+        if (next < n_deep) {
+            const uint64_t idle = __ballot(!active) & kLeads;
+            if (idle) {
+                const uint32_t idx = next + (uint32_t)__popcll(idle & ((1ull << (lane & ~3)) - 1ull));
+                if (!active && idx < n_deep) {
+                    const f4 A = W.ro[idx], D = W.rd[idx];
+                    id = __float_as_uint(D.w);
+                    any = id >= 64u;
+                    o = xyz(A), d = xyz(D), tmax = A.w;
+                    bt = kINF, bk = -1;
+                    if (!any) {
+                        const unsigned long long key = W.best[id];
+                        if (key != ~0ull) bt = __uint_as_float((uint32_t)(key >> 32)), bk = (int)(uint32_t)key;
+                    }
+                    inv = rcp3(d);
+                    node = 0, sp = 0;
+                    active = true;
+                }
+                next += (uint32_t)__popcll(idle);
+            }
+        }
+        if (!__ballot(active)) break;
+        if (!active) continue;
+        // ---- one node: child c on lane c; lim = the quad's best t (closest hits) or tmax
+        f4 lo, hi;
+        if (node < ntop) {
+            lo = top[8 * node + c], hi = top[8 * node + 4 + c];
+        } else {
+            lo = ldg4(P.bvh4, 8 * (size_t)node + c), hi = ldg4(P.bvh4, 8 * (size_t)node + 4 + c);
+        }
+        const int cidx = __float_as_int(lo.w), ccnt = __float_as_int(hi.w);
+        float lim = any ? tmax : __uint_as_float(group_min32<4>(__float_as_uint(bt)));   // t >= 0: bits order
+        const float e = ccnt >= 0 ? bvh_enter(lo, hi, o, inv, lim) : __builtin_inff();
+        bool done = false;
+        if (any) {
+            bool oc = false;
+            if (ccnt > 0 && e != __builtin_inff()) oc = deep_leaf<true>(P, cidx, ccnt, o, d, tmax, bt, bk);
+            done = group_or32<4>(oc ? 1u : 0u) != 0u;
+            if (done && c == 0) atomicOr(&W.occ[id & 63u], 1u << ((id >> 6) - 1u));
+        } else {
+            if (ccnt > 0 && e != __builtin_inff()) {
+                (void)deep_leaf<false>(P, cidx, ccnt, o, d, kINF, bt, bk);
+                lim = __builtin_fminf(lim, bt);   // this lane's leaf may have closed in
+            }
+            lim = __uint_as_float(group_min32<4>(__float_as_uint(lim)));
+        }
+        if (!done) {
+            const bool inner = ccnt == 0 && e <= lim;   // interior child still overlapping [0, lim]
+            const uint32_t nkey = inner ? ((__float_as_uint(e) & ~3u) | (uint32_t)c) : ~0u;
+            const uint32_t nmin = group_min32<4>(nkey);
+            if (nmin != ~0u) {
+                const bool nearest = nkey == nmin;
+                const uint32_t m4 = (uint32_t)(__ballot(inner && !nearest) >> (lane & ~3)) & 0xfu;
+                if (inner && !nearest) qs[(sp + __popc(m4 & ((1u << c) - 1u))) * 16] = (SE)cidx;
+                sp += __popc(m4);
+                node = (int)group_or32<4>(nearest ? (uint32_t)cidx : 0u);
+            } else if (sp == 0) {
+                done = true;
+            } else {
+                node = (int)qs[(--sp) * 16];
+            }
+        }
+        if (done) {
+            if (!any) {   // the quad's closest hit: the smallest (t bits, index) of the lanes
+                const uint64_t key = bk >= 0 ? ((uint64_t)__float_as_uint(bt) << 32) | (uint32_t)bk : ~0ull;
+                const uint64_t kmin = group_min64<4>(key);
+                if (c == 0 && kmin != ~0ull) W.best[id] = kmin;
+            }
+            active = false;
+        }
+    }
+}
+
+// After merged_trace<NL, true> over the small objects: rank the rays whose segment still
+// reaches the BVH root (the same root test as phase A's queueing, k_trace_2a_coop) into the
+// wave's scratch, walk them, and return the merged records.  Must be called by every lane.
+template <int NL, typename SE>
+__device__ __forceinline__ void deep_pass(const KParams& P, const f4* top, int ntop, SE* stk, MergedWave<NL>& W,
+                                          int lane, const f4 (&root)[4], bool ext, v3 o, v3 d, uint32_t shm,
+                                          const v3 (&so)[NL + 1], const v3 (&sd)[NL + 1], const float (&stm)[NL + 1],
+                                          unsigned long long& best, uint32_t& occ) {
+    constexpr int R = 1 + NL;
+    bool need[R];
+    const float bt = best == ~0ull ? kINF : __uint_as_float((uint32_t)(best >> 32));
+    need[0] = ext && root_overlap(root[0], root[1], root[2], root[3], o, rcp3(d), bt);
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+        need[1 + l] = ((shm & ~occ) >> l & 1u) && root_overlap(root[0], root[1], root[2], root[3], so[l], rcp3(sd[l]), stm[l]);
+    wave_sync();   // the last pair pass's reads of W.ro / W.rd are done
+    uint32_t tot = 0;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const uint64_t m = __ballot(need[q]);
+        if (need[q]) {
+            const uint32_t at = tot + lanemask_rank(m);
+            const v3 ro = q == 0 ? o : so[q - 1], rd = q == 0 ? d : sd[q - 1];
+            W.ro[at] = make_float4(ro.x, ro.y, ro.z, q == 0 ? kINF : stm[q - 1]);
+            W.rd[at] = make_float4(rd.x, rd.y, rd.z, __uint_as_float((uint32_t)(q * 64 + lane)));
+        }
+        tot += (uint32_t)__popcll(m);
+    }
+    if (tot == 0) return;
+    wave_sync();
+    wave_deep_walk<NL, SE>(P, top, ntop, stk, W, lane, tot);
+    wave_sync();
+    best = W.best[lane];
+    occ = W.occ[lane];
+}
+
+// LDS of k_step_merged<..., BVH = true> (bytes; the f4 regions 16-aligned): the small
+// objects' triangles (KParams::stri), the object and light tables, the first ntop 4-wide
+// BVH nodes, one MergedWave per wave, then 16 quad stacks of bvh4_stack 16-bit entries per
+// wave (use_step_bvh: at most 65,536 nodes).
+struct BvhStepLayout {
+    uint32_t tri, obj, light, top, wave, stack, total;
+    int ntop;
+};
+__host__ __device__ inline BvhStepLayout bvh_step_layout(const KParams& P, uint32_t wave_bytes) {
+    BvhStepLayout B;
+    B.tri = 0;
+    B.obj = 48u * (uint32_t)P.n_stri;
+    B.light = B.obj + (uint32_t)sizeof(DObj) * (uint32_t)P.n_objs;
+    B.top = (B.light + (uint32_t)sizeof(DLight) * (uint32_t)P.n_lights + 15u) & ~15u;
+    B.ntop = P.bvh4_nodes < (int)kBvhTopNodes ? P.bvh4_nodes : (int)kBvhTopNodes;
+    B.wave = B.top + 128u * (uint32_t)B.ntop;
+    B.stack = B.wave + (kBlock / 64) * wave_bytes;
+    B.total = B.stack + (kBlock / 64) * 16u * (uint32_t)P.bvh4_stack * 2u;
+    return B;
 }
 
 // ------------------------------------------------- two-level trace, phase A ----
@@ -489,39 +701,89 @@ hipError_t launch_trace_2a_coop(const KParams& P, const uint32_t* list, const ui
 // (redundantly, results identical) and the group shares the traces (group_trace).  Either
 // way, with few slots per GPU (a pixel shard of a multi-GPU frame) this puts more, shorter
 // waves on every SIMD.
-template <int INTEG, int NL, int SPW, int G, bool LANE>
-__global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
+// BVH: two-level scenes (use_step_bvh: C4) — the small objects' triangles in LDS and traced
+// by merged_trace with original-index keys, the rest by the wave's BVH walk (deep_pass); the
+// hit triangle's shading data from global memory.  Same path code otherwise.
+#ifndef XRT_BVH_WAVES
+#define XRT_BVH_WAVES 2
+#endif
+template <int INTEG, int NL, int SPW, int G, bool LANE, bool BVH>
+__global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void k_step_merged(
     const KParams* __restrict__ Pp, const StepObjs SO, const uint32_t* __restrict__ list,
     const uint32_t* __restrict__ count, uint32_t* __restrict__ out, uint32_t* out_count, uint32_t* zero_count,
     uint32_t* req_count, uint32_t visits) {
     constexpr int NW = 6 + 2 * NL;   // most words one segment draws (see the header)
+    static_assert(!BVH || (G == 1 && !LANE), "two-level scenes trace by pair passes");
     const KParams& P = *Pp;
     extern __shared__ __attribute__((aligned(16))) f4 lds_m[];
     char* lb = reinterpret_cast<char*>(lds_m);
-    const StepLayout Lo = step_layout(P);
-    LScene L;
-    L.tri = reinterpret_cast<const f4*>(lb + Lo.tri);
-    L.tng = reinterpret_cast<const f4*>(lb + Lo.tng);
-    L.nrm = reinterpret_cast<const f4*>(lb + Lo.nrm);
-    L.box = reinterpret_cast<const DObjBox*>(lb + Lo.box);
-    L.sph = reinterpret_cast<const f4*>(lb + Lo.sph);
-    L.bx = reinterpret_cast<const f4*>(lb + Lo.bx);
-    L.obj = reinterpret_cast<const DObj*>(lb + Lo.obj);
-    L.light = reinterpret_cast<const DLight*>(lb + Lo.light);
-    L.sobj = reinterpret_cast<const int*>(lb + Lo.sobj);
     const int tid = threadIdx.x, lane = tid & 63;
-    const DObjPlane* lplane = reinterpret_cast<const DObjPlane*>(lb + merged_plane_off(Lo));
-    MergedWave<NL>& W = reinterpret_cast<MergedWave<NL>*>(lb + merged_wave_off(P, Lo))[tid >> 6];
-    static_assert(sizeof(MergedWave<NL>) >= kMT * 4, "the wave's trace scratch doubles as the refill buffer");
-    lds_copy(const_cast<f4*>(L.tri), P.tri, 3 * P.n_tris, tid);
-    lds_copy(const_cast<f4*>(L.tng), P.tri_ng, P.n_tris, tid);
-    lds_copy(const_cast<f4*>(L.nrm), P.tri_nrm, 3 * P.n_tris, tid);
-    lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
-    lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid);
-    if (LANE) {
-        lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid);
-        lds_copy(const_cast<DObjPlane*>(lplane), P.obj_plane, P.n_objs, tid);
+    LScene L;
+    const DObjPlane* lplane = nullptr;
+    MergedWave<NL>* Wp;
+    const f4* top = nullptr;   // BVH: the first ntop 4-wide nodes
+    uint16_t* stk = nullptr;   // BVH: this wave's quad stacks
+    int ntop = 0;
+    f4 root[4];                // BVH: the binary root node (deep_pass's root test)
+    if constexpr (BVH) {
+        const BvhStepLayout Bl = bvh_step_layout(P, (uint32_t)sizeof(MergedWave<NL>));
+        L.tri = reinterpret_cast<const f4*>(lb + Bl.tri);
+        L.obj = reinterpret_cast<const DObj*>(lb + Bl.obj);
+        L.light = reinterpret_cast<const DLight*>(lb + Bl.light);
+        top = reinterpret_cast<const f4*>(lb + Bl.top);
+        ntop = Bl.ntop;
+        Wp = reinterpret_cast<MergedWave<NL>*>(lb + Bl.wave);
+        stk = reinterpret_cast<uint16_t*>(lb + Bl.stack) + (tid >> 6) * 16 * P.bvh4_stack;
+        lds_copy(const_cast<f4*>(L.tri), P.stri, 3 * P.n_stri, tid);
+        lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
+        lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid);
+        lds_copy(const_cast<f4*>(top), P.bvh4, 8 * ntop, tid);
+        root[0] = ldg4(P.bvh_node, 0), root[1] = ldg4(P.bvh_node, 1), root[2] = ldg4(P.bvh_node, 2);
+        root[3] = ldg4(P.bvh_node, 3);
+    } else {
+        const StepLayout Lo = step_layout(P);
+        L.tri = reinterpret_cast<const f4*>(lb + Lo.tri);
+        L.tng = reinterpret_cast<const f4*>(lb + Lo.tng);
+        L.nrm = reinterpret_cast<const f4*>(lb + Lo.nrm);
+        L.box = reinterpret_cast<const DObjBox*>(lb + Lo.box);
+        L.sph = reinterpret_cast<const f4*>(lb + Lo.sph);
+        L.bx = reinterpret_cast<const f4*>(lb + Lo.bx);
+        L.obj = reinterpret_cast<const DObj*>(lb + Lo.obj);
+        L.light = reinterpret_cast<const DLight*>(lb + Lo.light);
+        L.sobj = reinterpret_cast<const int*>(lb + Lo.sobj);
+        lplane = reinterpret_cast<const DObjPlane*>(lb + merged_plane_off(Lo));
+        Wp = reinterpret_cast<MergedWave<NL>*>(lb + merged_wave_off(P, Lo));
+        lds_copy(const_cast<f4*>(L.tri), P.tri, 3 * P.n_tris, tid);
+        lds_copy(const_cast<f4*>(L.tng), P.tri_ng, P.n_tris, tid);
+        lds_copy(const_cast<f4*>(L.nrm), P.tri_nrm, 3 * P.n_tris, tid);
+        lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
+        lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid);
+        if (LANE) {
+            lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid);
+            lds_copy(const_cast<DObjPlane*>(lplane), P.obj_plane, P.n_objs, tid);
+        }
     }
+    MergedWave<NL>& W = Wp[tid >> 6];
+    static_assert(sizeof(MergedWave<NL>) >= kMT * 4, "the wave's trace scratch doubles as the refill buffer");
+    // the hit triangle's records: LDS (the whole scene is there) or, two-level, global memory
+    // (hk is then the triangle's original index)
+    auto tri_rec = [&](int i) -> f4 {
+        if constexpr (BVH) return ldg4(P.tri, i);
+        else return L.tri[i];
+    };
+    auto tri_ng_at = [&](int i) -> v3 {
+        if constexpr (BVH) return xyz(ldg4(P.tri_ng, i));
+        else return xyz(L.tng[i]);
+    };
+    auto tri_ns_at = [&](int i, float u, float v) -> v3 {
+        if constexpr (BVH) {
+            const float w = 1.0f - u - v;
+            return xyz(ldg4(P.tri_nrm, 3 * (size_t)i)) * w + xyz(ldg4(P.tri_nrm, 3 * (size_t)i + 1)) * u +
+                   xyz(ldg4(P.tri_nrm, 3 * (size_t)i + 2)) * v;
+        } else {
+            return tri_ns_l(L, i, u, v);
+        }
+    };
     __syncthreads();
 #ifdef XRT_PHASE_CLOCK
     uint64_t ph_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -650,10 +912,14 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
             MPH_MARK(0);
             unsigned long long best;
             uint32_t occ;
-            if constexpr (!LANE)
+            if constexpr (BVH) {
+                merged_trace<NL, true>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ PH_TARGS);
+                deep_pass<NL, uint16_t>(P, top, ntop, stk, W, lane, root, ext_now, o, d, shm, so, sd, stm, best, occ);
+            } else if constexpr (!LANE) {
                 merged_trace<NL>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ PH_TARGS);
-            else
+            } else {
                 group_trace<NL, G>(P.n_objs, L, lplane, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
+            }
             MPH_MARK(1);
             resolve(occ);
             if (vis > 0) rng.take();   // the words prefetched at the end of the previous segment
@@ -664,12 +930,12 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                 float ht = kINF, hu = 0.0f, hv = 0.0f;
                 if (best != ~0ull) {
                     hk = (int)(uint32_t)best;
-                    (void)ray_tri(o, d, xyz(L.tri[3 * hk]), xyz(L.tri[3 * hk + 1]), xyz(L.tri[3 * hk + 2]), ht, hu,
-                                  hv);
-                    obj = __float_as_int(L.tri[3 * hk].w);
+                    const f4 ta = tri_rec(3 * hk);
+                    (void)ray_tri(o, d, xyz(ta), xyz(tri_rec(3 * hk + 1)), xyz(tri_rec(3 * hk + 2)), ht, hu, hv);
+                    obj = __float_as_int(ta.w);
                 }
                 v3 pos = mk(0, 0, 0), ng = mk(0, 0, 0);
-                if (hk >= 0) pos = ray_at(o, d, ht), ng = xyz(L.tng[hk]);
+                if (hk >= 0) pos = ray_at(o, d, ht), ng = tri_ng_at(hk);
                 bool ended = false, alive = false;
                 MPH_MARK(8);
                 if (INTEG == XRT_INTEGRATOR_DIRECT) {
@@ -678,7 +944,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                         rad = mk((float)0.18, (float)0.18, (float)0.18);
                         ended = true;
                     } else if (L.obj[obj].light >= 0) {
-                        rad = light_Le(L.light[L.obj[obj].light], tri_ns_l(L, hk, hu, hv), d);
+                        rad = light_Le(L.light[L.obj[obj].light], tri_ns_at(hk, hu, hv), d);
                         ended = true;
                     } else {
                         alive = true;
@@ -697,7 +963,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                         }
                         if (alive && L.obj[obj].light >= 0) {
                             if (depth == 0)
-                                rad = rad + thr * light_Le(L.light[L.obj[obj].light], tri_ns_l(L, hk, hu, hv), d);
+                                rad = rad + thr * light_Le(L.light[L.obj[obj].light], tri_ns_at(hk, hu, hv), d);
                             alive = false, ended = true;
                         }
                     }
@@ -743,7 +1009,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
                         const bool lamb = ob.material == 1;
                         if (lamb) {
                             v3 dpdu, dpdv;
-                            onb(tri_ns_l(L, hk, hu, hv), dpdu, dpdv);
+                            onb(tri_ns_at(hk, hu, hv), dpdu, dpdv);
                             nd = lambert_sample_f(ng, dpdu, dpdv, rng);
                         }
                         const float cosv = smax(0.0f, dot(nd, ng));
@@ -782,10 +1048,14 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_merged(
         if (__ballot(shm != 0)) {
             unsigned long long best;
             uint32_t occ;
-            if constexpr (!LANE)
+            if constexpr (BVH) {
+                merged_trace<NL, true>(SO, L, W, lane, false, o, d, shm, so, sd, stm, best, occ PH_TARGS);
+                deep_pass<NL, uint16_t>(P, top, ntop, stk, W, lane, root, false, o, d, shm, so, sd, stm, best, occ);
+            } else if constexpr (!LANE) {
                 merged_trace<NL>(SO, L, W, lane, false, o, d, shm, so, sd, stm, best, occ PH_TARGS);
-            else
+            } else {
                 group_trace<NL, G>(P.n_objs, L, lplane, lane, false, o, d, shm, so, sd, stm, best, occ);
+            }
             resolve(occ);
         }
         MPH_MARK(5);
@@ -883,17 +1153,33 @@ bool use_step_merged(const KParams& P) {
            !exp_env("XRT_NO_MERGED") && step_merged_lds_bytes(P) <= kStepLds;
 }
 
+// The merged schedule for two-level scenes (C4): k_step_merged<..., BVH = true>.  The small
+// objects must be traceable by pair passes (KParams::sstep: at most kMergedMaxObjs objects,
+// det_bounded), the 4-wide BVH's node indices fit the 16-bit quad stacks, and at least one
+// area light (the kernel is instantiated for 1..kMaxLights).
+bool use_step_bvh(const KParams& P) {
+    return P.scene_kind == SCN_TRI && P.two_level && P.sstep && P.det_bounded && P.bvh4 && P.bvh_node &&
+           P.bvh4_nodes <= 0x10000 && P.bvh4_stack > 0 && P.bvh4_stack <= kBvh4Stack && P.n_lights >= 1 &&
+           P.n_lights <= kMaxLights &&
+           (P.integrator == XRT_INTEGRATOR_DIRECT || (P.integrator == XRT_INTEGRATOR_GI && P.max_depth > 0)) &&
+           !exp_env("XRT_NO_STEP_BVH") && step_merged_lds_bytes(P) <= kStepLds;
+}
+
 uint32_t step_merged_draws(const KParams& P) { return 6u + 2u * (uint32_t)P.n_lights; }
 
-size_t step_merged_lds_bytes(const KParams& P) {
-    size_t w = 0;
-    switch (P.n_lights) {
-        case 0: w = sizeof(MergedWave<0>); break;
-        case 1: w = sizeof(MergedWave<1>); break;
-        case 2: w = sizeof(MergedWave<2>); break;
-        case 3: w = sizeof(MergedWave<3>); break;
-        default: w = sizeof(MergedWave<4>); break;
+static size_t merged_wave_bytes(int n_lights) {
+    switch (n_lights) {
+        case 0: return sizeof(MergedWave<0>);
+        case 1: return sizeof(MergedWave<1>);
+        case 2: return sizeof(MergedWave<2>);
+        case 3: return sizeof(MergedWave<3>);
+        default: return sizeof(MergedWave<4>);
     }
+}
+
+size_t step_merged_lds_bytes(const KParams& P) {
+    const size_t w = merged_wave_bytes(P.n_lights);
+    if (P.two_level) return bvh_step_layout(P, (uint32_t)w).total;
     return merged_wave_off(P, step_layout(P)) + (kBlock / 64) * w;
 }
 
@@ -913,7 +1199,7 @@ void build_step_objs(const DObjBox* boxes, const DObjPlane* planes, int n, StepO
     }
 }
 
-template <int INTEG, int SPW, int G, bool LANE>
+template <int INTEG, int SPW, int G, bool LANE, bool BVH = false>
 static void launch_merged_i(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                             const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
                             uint32_t* req_count, uint32_t visits, uint32_t part_live, size_t lds, hipStream_t st) {
@@ -922,14 +1208,23 @@ static void launch_merged_i(const KParams& P, const KParams* dP, const StepObjs&
     const uint32_t per_block = (kBlock / 64) * SPW;
     const uint32_t blocks = P.n_part * ((std::min(part_live, P.part_cap) + per_block - 1) / per_block);
 #define XRT_LAUNCH_MERGED(NLV)                                                                                       \
-    hipLaunchKernelGGL((k_step_merged<INTEG, NLV, SPW, G, LANE>), dim3(blocks), dim3(kBlock), lds, st, dP, SO, list, count, \
-                       out, out_count, zero, req_count, visits)
-    switch (P.n_lights) {
-        case 0: XRT_LAUNCH_MERGED(0); break;
-        case 1: XRT_LAUNCH_MERGED(1); break;
-        case 2: XRT_LAUNCH_MERGED(2); break;
-        case 3: XRT_LAUNCH_MERGED(3); break;
-        default: XRT_LAUNCH_MERGED(4); break;
+    hipLaunchKernelGGL((k_step_merged<INTEG, NLV, SPW, G, LANE, BVH>), dim3(blocks), dim3(kBlock), lds, st, dP, SO, list, \
+                       count, out, out_count, zero, req_count, visits)
+    if constexpr (BVH) {   // use_step_bvh: 1..kMaxLights lights
+        switch (P.n_lights) {
+            case 1: XRT_LAUNCH_MERGED(1); break;
+            case 2: XRT_LAUNCH_MERGED(2); break;
+            case 3: XRT_LAUNCH_MERGED(3); break;
+            default: XRT_LAUNCH_MERGED(4); break;
+        }
+    } else {
+        switch (P.n_lights) {
+            case 0: XRT_LAUNCH_MERGED(0); break;
+            case 1: XRT_LAUNCH_MERGED(1); break;
+            case 2: XRT_LAUNCH_MERGED(2); break;
+            case 3: XRT_LAUNCH_MERGED(3); break;
+            default: XRT_LAUNCH_MERGED(4); break;
+        }
     }
 #undef XRT_LAUNCH_MERGED
 }
@@ -963,6 +1258,18 @@ static void launch_merged_spw(const KParams& P, const KParams* dP, const StepObj
                               hipStream_t st) {
     const bool group = P.n_tris <= 64 && !(P.rflags & XRT_FLAG_NO_GROUP);   // group trace: 64-bit triangle masks
     const bool lane64 = group && exp_env("XRT_LANE_TRACE");   // experiment: per-lane traces, full waves
+    if (P.two_level) {   // use_step_bvh (never group traces: n_tris > 64)
+#define XRT_BVH_CASE(SPWV) \
+    launch_merged_i<INTEG, SPWV, 1, false, true>(P, dP, *P.sstep, list, count, out, out_count, zero, req_count, visits, \
+                                                 part_live, lds, st)
+        switch (step_merged_spw(P, live)) {
+            case 64: XRT_BVH_CASE(64); break;
+            case 32: XRT_BVH_CASE(32); break;
+            default: XRT_BVH_CASE(16); break;
+        }
+#undef XRT_BVH_CASE
+        return;
+    }
 #define XRT_MERGED_CASE(SPWV, GV, LV) \
     launch_merged_i<INTEG, SPWV, GV, LV>(P, dP, SO, list, count, out, out_count, zero, req_count, visits, part_live, lds, st)
     switch (step_merged_spw(P, live)) {

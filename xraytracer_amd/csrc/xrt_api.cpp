@@ -807,8 +807,10 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     // compaction and refill requests) when the scene fits, in its merged-trace form for small
     // triangle scenes; else the multi-pass wavefront (k_shade, then k_trace streaming the
     // scene through LDS tiles; k_shade refills its slots' rings in-line).
-    const bool fused = !(p->flags & XRT_FLAG_WAVEFRONT) && step_lds_bytes(P) != 0;
-    const bool merged = fused && !(p->flags & XRT_FLAG_NO_MERGED) && use_step_merged(P);
+    // Two-level scenes (C4) take the merged kernel with the wave's own BVH walk.
+    const bool bvh = !(p->flags & (XRT_FLAG_WAVEFRONT | XRT_FLAG_NO_MERGED)) && use_step_bvh(P);
+    const bool fused = bvh || (!(p->flags & XRT_FLAG_WAVEFRONT) && step_lds_bytes(P) != 0);
+    const bool merged = bvh || (fused && !(p->flags & XRT_FLAG_NO_MERGED) && use_step_merged(P));
     // live-list partitions (a multiple of the 8 XCDs): every wave appends to its partition's
     // counters once per launch, so more partitions mean less atomic contention (64 -> 256:
     // C4 -14%, C2 -4.5%).  The merged schedule (64 segments per launch) is fastest with
@@ -1044,6 +1046,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     S.segments = hs[0], S.shadow_rays = hs[1], S.draws = hs[2], S.rejected = hs[3], S.stalled = hs[4];
     S.rng_twists = hs[7];
     S.schedule = !fused ? XRT_SCHED_WAVEFRONT
+                 : bvh    ? XRT_SCHED_STEP_BVH
                  : merged ? XRT_SCHED_STEP_MERGED
                  : use_step_tri(P) ? XRT_SCHED_STEP_TRI : XRT_SCHED_STEP;
     S.partitions = P.n_part;
