@@ -389,8 +389,17 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const D
 // index) against a ray: closest hit as the (t, original index) minimum, or any occluder hit
 // below tmax.  The loads of the whole leaf are issued before the first test.  Mesh::
 // rayTriangleIntersect's decisions via ray_tri_nb (two-level scenes are det_bounded).
+#ifndef XRT_PARK
+#define XRT_PARK 0   // experiment: park slots with deep rays and walk the pool in batches (C4 slower: DESIGN.md §3)
+#endif
+#ifndef XRT_PARK_EIGHTHS
+#define XRT_PARK_EIGHTHS 3   // ... once this many eighths of the wave's slots are parked
+#endif
+#ifndef XRT_BVH_TOP
+#define XRT_BVH_TOP 64   // breadth-first top nodes of the 4-wide BVH kept in LDS (at most; kStepLds bounds it)
+#endif
 #ifndef XRT_DEEP_LEAF_BATCH
-#define XRT_DEEP_LEAF_BATCH 4   // triangles whose loads are issued together (1, 2 or 4): registers vs latency
+#define XRT_DEEP_LEAF_BATCH 2   // triangles whose loads are issued together (1, 2 or 4): registers vs latency
 #endif
 template <bool ANY>
 __device__ __forceinline__ bool deep_leaf(const KParams& P, int first, int count, v3 o, v3 d, float tmax, float& bt,
@@ -425,12 +434,14 @@ __device__ __forceinline__ bool deep_leaf(const KParams& P, int first, int count
     return occ;
 }
 
-// The walk of n_deep ranked rays W.ro / W.rd (w: tmax resp. the ray id q * 64 + lane).
-// top: the first ntop 4-wide nodes in LDS; stk: this wave's 16 quad stacks (stride 16).
-// Must be called by every lane of the wave.
-template <int NL, typename SE>
-__device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, int ntop, SE* stk, MergedWave<NL>& W,
-                                               int lane, uint32_t n_deep) {
+// The walk of n_deep ranked rays ray_o / ray_d (w: tmax resp. the ray id q * 64 + lane; q = 0:
+// extension ray, closest hit from the key best[lane]; 1 + l: shadow ray l, occlusion bit l of
+// occ[lane]).  top: the first ntop 4-wide nodes in LDS; stk: this wave's 16 quad stacks
+// (stride 16).  Must be called by every lane of the wave.
+template <typename SE>
+__device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, int ntop, SE* stk, const f4* ray_o,
+                                               const f4* ray_d, unsigned long long* best, uint32_t* occ, int lane,
+                                               uint32_t n_deep) {
     constexpr uint64_t kLeads = 0x1111111111111111ull;   // lane 0 of every quad
     const int c = lane & 3;
     SE* qs = stk + (lane >> 2);
@@ -440,19 +451,22 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
     int node = 0, sp = 0, bk = -1;
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0), inv = mk(0, 0, 0);
     float tmax = 0.0f, bt = kINF;
+#ifdef XRT_EXPERIMENTS
+    uint32_t niter = 0, nsteps = 0;
+#endif
     while (true) {
         if (next < n_deep) {
             const uint64_t idle = __ballot(!active) & kLeads;
             if (idle) {
                 const uint32_t idx = next + (uint32_t)__popcll(idle & ((1ull << (lane & ~3)) - 1ull));
                 if (!active && idx < n_deep) {
-                    const f4 A = W.ro[idx], D = W.rd[idx];
+                    const f4 A = ray_o[idx], D = ray_d[idx];
                     id = __float_as_uint(D.w);
                     any = id >= 64u;
                     o = xyz(A), d = xyz(D), tmax = A.w;
                     bt = kINF, bk = -1;
                     if (!any) {
-                        const unsigned long long key = W.best[id];
+                        const unsigned long long key = best[id];
                         if (key != ~0ull) bt = __uint_as_float((uint32_t)(key >> 32)), bk = (int)(uint32_t)key;
                     }
                     inv = rcp3(d);
@@ -463,6 +477,10 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
             }
         }
         if (!__ballot(active)) break;
+#ifdef XRT_EXPERIMENTS
+        ++niter;
+        nsteps += (uint32_t)__popcll(__ballot(active) & kLeads);
+#endif
         if (!active) continue;
         // ---- one node: child c on lane c; lim = the quad's best t (closest hits) or tmax
         f4 lo, hi;
@@ -479,7 +497,7 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
             bool oc = false;
             if (ccnt > 0 && e != __builtin_inff()) oc = deep_leaf<true>(P, cidx, ccnt, o, d, tmax, bt, bk);
             done = group_or32<4>(oc ? 1u : 0u) != 0u;
-            if (done && c == 0) atomicOr(&W.occ[id & 63u], 1u << ((id >> 6) - 1u));
+            if (done && c == 0) atomicOr(&occ[id & 63u], 1u << ((id >> 6) - 1u));
         } else {
             if (ccnt > 0 && e != __builtin_inff()) {
                 (void)deep_leaf<false>(P, cidx, ccnt, o, d, kINF, bt, bk);
@@ -507,11 +525,18 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
             if (!any) {   // the quad's closest hit: the smallest (t bits, index) of the lanes
                 const uint64_t key = bk >= 0 ? ((uint64_t)__float_as_uint(bt) << 32) | (uint32_t)bk : ~0ull;
                 const uint64_t kmin = group_min64<4>(key);
-                if (c == 0 && kmin != ~0ull) W.best[id] = kmin;
+                if (c == 0 && kmin != ~0ull) best[id] = kmin;
             }
             active = false;
         }
     }
+#ifdef XRT_EXPERIMENTS
+    if (lane == 0) {
+        atomicAdd(P.stats + 38, (unsigned long long)n_deep), atomicAdd(P.stats + 39, (unsigned long long)nsteps);
+        atomicAdd(P.stats + 37, (unsigned long long)niter), atomicMax(P.stats + 36, (unsigned long long)niter);
+        atomicAdd(P.stats + 35, 1ull);
+    }
+#endif
 }
 
 // After merged_trace<NL, true> over the small objects: rank the rays whose segment still
@@ -544,18 +569,58 @@ __device__ __forceinline__ void deep_pass(const KParams& P, const f4* top, int n
     }
     if (tot == 0) return;
     wave_sync();
-    wave_deep_walk<NL, SE>(P, top, ntop, stk, W, lane, tot);
+    wave_deep_walk<SE>(P, top, ntop, stk, W.ro, W.rd, W.best, W.occ, lane, tot);
     wave_sync();
     best = W.best[lane];
     occ = W.occ[lane];
 }
 
+// Parking.  A wave's deep rays per visit are few (about 6 of its ~90 rays at C4) and their
+// walks differ in length, so walking them every visit (deep_pass) makes the wave wait for the
+// longest of a handful of walks each time.  Instead a slot whose rays still reach the BVH
+// after the small objects is parked: its rays join the wave's pool (Q: the ray records, the
+// slot's small-object closest-hit key and occlusion bits), it skips the visits that follow
+// (its path state stays in registers, untouched), and when enough slots are parked the wave
+// walks the whole pool at once — 16 quads fetching rays dynamically, bound by the pool's
+// total work rather than by one walk — and the parked slots resume with the merged results.
+// The slot's draws and sums happen in the same order whatever visit it resumes in.
+// Returns whether this lane parked.  Must be called by every lane (pool_n is wave-uniform).
+template <int NL>
+__device__ __forceinline__ bool deep_park(MergedWave<NL>& Q, uint32_t& pool_n, int lane, const f4 (&root)[4], bool ext,
+                                          v3 o, v3 d, uint32_t shm, const v3 (&so)[NL + 1], const v3 (&sd)[NL + 1],
+                                          const float (&stm)[NL + 1], unsigned long long best, uint32_t occ) {
+    constexpr int R = 1 + NL;
+    bool need[R];
+    const float bt = best == ~0ull ? kINF : __uint_as_float((uint32_t)(best >> 32));
+    need[0] = ext && root_overlap(root[0], root[1], root[2], root[3], o, rcp3(d), bt);
+    bool park = need[0];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+        need[1 + l] = ((shm & ~occ) >> l & 1u) && root_overlap(root[0], root[1], root[2], root[3], so[l], rcp3(sd[l]), stm[l]);
+        park |= need[1 + l];
+    }
+    if (park) Q.best[lane] = best, Q.occ[lane] = occ;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const uint64_t m = __ballot(need[q]);
+        if (need[q]) {
+            const uint32_t at = pool_n + lanemask_rank(m);
+            const v3 ro = q == 0 ? o : so[q - 1], rd = q == 0 ? d : sd[q - 1];
+            Q.ro[at] = make_float4(ro.x, ro.y, ro.z, q == 0 ? kINF : stm[q - 1]);
+            Q.rd[at] = make_float4(rd.x, rd.y, rd.z, __uint_as_float((uint32_t)(q * 64 + lane)));
+        }
+        pool_n += (uint32_t)__popcll(m);
+    }
+    return park;
+}
+
 // LDS of k_step_merged<..., BVH = true> (bytes; the f4 regions 16-aligned): the small
 // objects' triangles (KParams::stri), the object and light tables, the first ntop 4-wide
-// BVH nodes, one MergedWave per wave, then 16 quad stacks of bvh4_stack 16-bit entries per
-// wave (use_step_bvh: at most 65,536 nodes).
+// BVH nodes, one MergedWave of trace scratch per wave, one MergedWave of parked rays per
+// wave (deep_park), then 16 quad stacks of bvh4_stack 16-bit entries per wave
+// (use_step_bvh: at most 65,536 nodes).
 struct BvhStepLayout {
-    uint32_t tri, obj, light, top, wave, stack, total;
+    uint32_t tri, obj, light, top, wave, pool, stack, total;
     int ntop;
 };
 __host__ __device__ inline BvhStepLayout bvh_step_layout(const KParams& P, uint32_t wave_bytes) {
@@ -564,9 +629,15 @@ __host__ __device__ inline BvhStepLayout bvh_step_layout(const KParams& P, uint3
     B.obj = 48u * (uint32_t)P.n_stri;
     B.light = B.obj + (uint32_t)sizeof(DObj) * (uint32_t)P.n_objs;
     B.top = (B.light + (uint32_t)sizeof(DLight) * (uint32_t)P.n_lights + 15u) & ~15u;
-    B.ntop = P.bvh4_nodes < (int)kBvhTopNodes ? P.bvh4_nodes : (int)kBvhTopNodes;
+    // as many of the top XRT_BVH_TOP nodes as the rest leaves room for within kStepLds
+    const uint32_t pool_bytes = XRT_PARK ? (kBlock / 64) * wave_bytes : 0u;
+    const uint32_t rest = B.top + (kBlock / 64) * wave_bytes + pool_bytes + (kBlock / 64) * 16u * (uint32_t)P.bvh4_stack * 2u;
+    const int fit = rest < kStepLds ? (int)((kStepLds - rest) / 128u) : 0;
+    B.ntop = P.bvh4_nodes < XRT_BVH_TOP ? P.bvh4_nodes : XRT_BVH_TOP;
+    B.ntop = B.ntop < fit ? B.ntop : fit;
     B.wave = B.top + 128u * (uint32_t)B.ntop;
-    B.stack = B.wave + (kBlock / 64) * wave_bytes;
+    B.pool = B.wave + (kBlock / 64) * wave_bytes;
+    B.stack = B.pool + pool_bytes;
     B.total = B.stack + (kBlock / 64) * 16u * (uint32_t)P.bvh4_stack * 2u;
     return B;
 }
@@ -702,11 +773,13 @@ hipError_t launch_trace_2a_coop(const KParams& P, const uint32_t* list, const ui
 // way, with few slots per GPU (a pixel shard of a multi-GPU frame) this puts more, shorter
 // waves on every SIMD.
 // BVH: two-level scenes (use_step_bvh: C4) — the small objects' triangles in LDS and traced
-// by merged_trace with original-index keys, the rest by the wave's BVH walk (deep_pass); the
-// hit triangle's shading data from global memory.  Same path code otherwise.
+// by merged_trace with original-index keys, the rest by the wave's BVH walk over the parked
+// slots' rays (deep_park); the hit triangle's shading data from global memory.  Same path
+// code otherwise.
 #ifndef XRT_BVH_WAVES
-#define XRT_BVH_WAVES 2
+#define XRT_BVH_WAVES 3   // 3 waves per SIMD (<= 168 VGPRs, no spills with two-triangle leaf batches)
 #endif
+
 template <int INTEG, int NL, int SPW, int G, bool LANE, bool BVH>
 __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void k_step_merged(
     const KParams* __restrict__ Pp, const StepObjs SO, const uint32_t* __restrict__ list,
@@ -721,6 +794,7 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
     LScene L;
     const DObjPlane* lplane = nullptr;
     MergedWave<NL>* Wp;
+    MergedWave<NL>* Qp = nullptr;   // BVH: the parked rays (deep_park)
     const f4* top = nullptr;   // BVH: the first ntop 4-wide nodes
     uint16_t* stk = nullptr;   // BVH: this wave's quad stacks
     int ntop = 0;
@@ -733,6 +807,7 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
         top = reinterpret_cast<const f4*>(lb + Bl.top);
         ntop = Bl.ntop;
         Wp = reinterpret_cast<MergedWave<NL>*>(lb + Bl.wave);
+        Qp = reinterpret_cast<MergedWave<NL>*>(lb + Bl.pool);
         stk = reinterpret_cast<uint16_t*>(lb + Bl.stack) + (tid >> 6) * 16 * P.bvh4_stack;
         lds_copy(const_cast<f4*>(L.tri), P.stri, 3 * P.n_stri, tid);
         lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
@@ -905,24 +980,51 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
         }
         __builtin_amdgcn_s_waitcnt(0);   // prologue loads done: the loop waits only on its own prefetches
         MPH_DECL
+        bool parked = false, p_ext = false, pf_pending = false;   // BVH: parked slot; its ext_now; words in pf[]
+        uint32_t pool_n = 0;                                      // BVH: rays in the pool (wave-uniform)
         for (uint32_t vis = 0; vis < visits; ++vis) {
             const bool act = live && !(st & ST_DONE) && g - rng.c >= (uint32_t)NW;
-            if (!__ballot(act || shm)) break;
-            const bool ext_now = act && ext;
+            if (!__ballot(act || shm || parked)) break;
+            bool ext_now = act && ext;
+            bool proceed = true;   // this lane's trace is complete: shade it this visit
             MPH_MARK(0);
             unsigned long long best;
             uint32_t occ;
-            if constexpr (BVH) {
+            if constexpr (BVH && !XRT_PARK) {
                 merged_trace<NL, true>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ PH_TARGS);
                 deep_pass<NL, uint16_t>(P, top, ntop, stk, W, lane, root, ext_now, o, d, shm, so, sd, stm, best, occ);
+            } else if constexpr (BVH) {
+                ext_now = ext_now && !parked;
+                merged_trace<NL, true>(SO, L, W, lane, ext_now, o, d, parked ? 0u : shm, so, sd, stm, best, occ PH_TARGS);
+                // a parked lane traced nothing this visit and passes no rays
+                const bool now = deep_park<NL>(Qp[tid >> 6], pool_n, lane, root, ext_now, o, d, parked ? 0u : shm, so,
+                                               sd, stm, best, occ);
+                if (now) parked = true, p_ext = ext_now;
+                proceed = !parked;
+                const uint32_t n_parked = (uint32_t)__popcll(__ballot(parked));
+                if (n_parked && (n_parked * 8u >= (uint32_t)SPW * XRT_PARK_EIGHTHS || vis + 1 == visits ||
+                                 !__ballot(proceed && (act || shm)))) {
+                    MergedWave<NL>& Q = Qp[tid >> 6];
+                    wave_sync();
+                    wave_deep_walk<uint16_t>(P, top, ntop, stk, Q.ro, Q.rd, Q.best, Q.occ, lane, pool_n);
+                    wave_sync();
+                    pool_n = 0;
+                    if (parked) {
+                        best = Q.best[lane], occ = Q.occ[lane];
+                        ext_now = p_ext;
+                        parked = false, proceed = true;
+                    }
+                    wave_sync();   // the pool is refilled from the next visit on
+                }
             } else if constexpr (!LANE) {
                 merged_trace<NL>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ PH_TARGS);
             } else {
                 group_trace<NL, G>(P.n_objs, L, lplane, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
             }
             MPH_MARK(1);
+            if (!proceed) continue;   // BVH: parked until the pool is walked
             resolve(occ);
-            if (vis > 0) rng.take();   // the words prefetched at the end of the previous segment
+            if (BVH ? pf_pending : vis > 0) rng.take();   // the words prefetched at the end of the previous segment
             MPH_MARK(2);
             if (ext_now) {
                 ++nseg;
@@ -1039,6 +1141,7 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
             }
             MPH_MARK(3);
             rng.prefetch(ring);   // unconditional; first read by take() after the next trace
+            pf_pending = true;
 #ifdef XRT_PHASE_CLOCK
             ++ph_vis;
 #endif
@@ -1155,12 +1258,12 @@ bool use_step_merged(const KParams& P) {
 
 // The merged schedule for two-level scenes (C4): k_step_merged<..., BVH = true>.  The small
 // objects must be traceable by pair passes (KParams::sstep: at most kMergedMaxObjs objects,
-// det_bounded), the 4-wide BVH's node indices fit the 16-bit quad stacks, and at least one
-// area light (the kernel is instantiated for 1..kMaxLights).
+// det_bounded), the 4-wide BVH's node indices fit the 16-bit quad stacks, one or two area
+// lights (the kernel's two pair-pass scratch buffers per wave must fit kStepLds).
 bool use_step_bvh(const KParams& P) {
     return P.scene_kind == SCN_TRI && P.two_level && P.sstep && P.det_bounded && P.bvh4 && P.bvh_node &&
            P.bvh4_nodes <= 0x10000 && P.bvh4_stack > 0 && P.bvh4_stack <= kBvh4Stack && P.n_lights >= 1 &&
-           P.n_lights <= kMaxLights &&
+           P.n_lights <= 2 &&
            (P.integrator == XRT_INTEGRATOR_DIRECT || (P.integrator == XRT_INTEGRATOR_GI && P.max_depth > 0)) &&
            !exp_env("XRT_NO_STEP_BVH") && step_merged_lds_bytes(P) <= kStepLds;
 }
@@ -1210,13 +1313,9 @@ static void launch_merged_i(const KParams& P, const KParams* dP, const StepObjs&
 #define XRT_LAUNCH_MERGED(NLV)                                                                                       \
     hipLaunchKernelGGL((k_step_merged<INTEG, NLV, SPW, G, LANE, BVH>), dim3(blocks), dim3(kBlock), lds, st, dP, SO, list, \
                        count, out, out_count, zero, req_count, visits)
-    if constexpr (BVH) {   // use_step_bvh: 1..kMaxLights lights
-        switch (P.n_lights) {
-            case 1: XRT_LAUNCH_MERGED(1); break;
-            case 2: XRT_LAUNCH_MERGED(2); break;
-            case 3: XRT_LAUNCH_MERGED(3); break;
-            default: XRT_LAUNCH_MERGED(4); break;
-        }
+    if constexpr (BVH) {   // use_step_bvh: 1 or 2 lights
+        if (P.n_lights == 1) XRT_LAUNCH_MERGED(1);
+        else XRT_LAUNCH_MERGED(2);
     } else {
         switch (P.n_lights) {
             case 0: XRT_LAUNCH_MERGED(0); break;

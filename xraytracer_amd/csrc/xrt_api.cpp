@@ -1031,8 +1031,8 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     HIPCHK(c, hipMemcpy(hs, P.stats, 40 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     if (hs[5] || hs[6]) std::fprintf(stderr, "[xrt] triangle tests: lane %llu wave %llu\n", hs[5], hs[6]);
     if (hs[38])   // experiment builds
-        std::fprintf(stderr, "[xrt] deep rays %llu node steps %llu wave iterations %llu max wave iterations %llu\n",
-                     hs[38], hs[39], hs[37], hs[36]);
+        std::fprintf(stderr, "[xrt] deep rays %llu node steps %llu wave iterations %llu max wave iterations %llu"
+                     " in-wave walks %llu\n", hs[38], hs[39], hs[37], hs[36], hs[8] || hs[9] ? 0ull : hs[35]);
     if (hs[8] || hs[9]) {   // -DXRT_PHASE_CLOCK experiment builds
         std::fprintf(stderr, "[xrt] phase cycles (sum over waves):");
         for (int q = 8; q < 16; ++q) std::fprintf(stderr, " %llu", hs[q]);
