@@ -398,6 +398,9 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const D
 #ifndef XRT_BVH_TOP
 #define XRT_BVH_TOP 64   // breadth-first top nodes of the 4-wide BVH kept in LDS (at most; kStepLds bounds it)
 #endif
+#ifndef XRT_DEEP_SPREAD
+#define XRT_DEEP_SPREAD 1   // a node's overlapped leaf triangles dealt over the quad's lanes
+#endif
 #ifndef XRT_DEEP_LEAF_BATCH
 #define XRT_DEEP_LEAF_BATCH 2   // triangles whose loads are issued together (1, 2 or 4): registers vs latency
 #endif
@@ -493,6 +496,53 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
         float lim = any ? tmax : __uint_as_float(group_min32<4>(__float_as_uint(bt)));   // t >= 0: bits order
         const float e = ccnt >= 0 ? bvh_enter(lo, hi, o, inv, lim) : __builtin_inff();
         bool done = false;
+#if XRT_DEEP_SPREAD
+        // The overlapped leaf children's triangles, dealt round robin over the quad's lanes
+        // (triangle j of the concatenated leaves to lane j % 4), so one leaf does not make one
+        // lane test its triangles serially while the other three wait.
+        bool oc = false;
+        {
+            const uint32_t mine = (ccnt > 0 && e != __builtin_inff()) ? (uint32_t)ccnt : 0u;
+            const uint32_t n0 = dpp32<0x00>(mine), n1 = dpp32<0x55>(mine), n2 = dpp32<0xAA>(mine), n3 = dpp32<0xFF>(mine);
+            const uint32_t f0 = dpp32<0x00>((uint32_t)cidx), f1 = dpp32<0x55>((uint32_t)cidx);
+            const uint32_t f2 = dpp32<0xAA>((uint32_t)cidx), f3 = dpp32<0xFF>((uint32_t)cidx);
+            const uint32_t p1 = n0, p2 = n0 + n1, p3 = p2 + n2, tot = p3 + n3;
+            constexpr int B = XRT_DEEP_LEAF_BATCH;
+            for (uint32_t j0 = (uint32_t)c; j0 < tot; j0 += 4u * B) {
+                f4 T[B][3];
+                bool ok[B];
+#pragma unroll
+                for (int b = 0; b < B; ++b) {
+                    const uint32_t j = j0 + 4u * (uint32_t)b;
+                    ok[b] = j < tot;
+                    if (ok[b]) {
+                        const uint32_t t = j < p1 ? f0 + j : j < p2 ? f1 + (j - p1) : j < p3 ? f2 + (j - p2) : f3 + (j - p3);
+                        const size_t i = 3 * (size_t)t;
+                        T[b][0] = ldg4(P.bvh_tri, i), T[b][1] = ldg4(P.bvh_tri, i + 1), T[b][2] = ldg4(P.bvh_tri, i + 2);
+                    }
+                }
+#pragma unroll
+                for (int b = 0; b < B; ++b) {
+                    if (!ok[b]) continue;
+                    if (any && T[b][1].w == 0.0f) continue;   // area-light objects never occlude
+                    float t;
+                    if (!ray_tri_nb(o, d, xyz(T[b][0]), xyz(T[b][1]), xyz(T[b][2]), t)) continue;
+                    if (any) {
+                        oc |= t < tmax;
+                    } else {
+                        const int k = __float_as_int(T[b][2].w);
+                        if (t < bt || (t == bt && k < bk)) bt = t, bk = k;
+                    }
+                }
+            }
+        }
+        if (any) {
+            done = group_or32<4>(oc ? 1u : 0u) != 0u;
+            if (done && c == 0) atomicOr(&occ[id & 63u], 1u << ((id >> 6) - 1u));
+        } else {
+            lim = __uint_as_float(group_min32<4>(__float_as_uint(__builtin_fminf(lim, bt))));
+        }
+#else
         if (any) {
             bool oc = false;
             if (ccnt > 0 && e != __builtin_inff()) oc = deep_leaf<true>(P, cidx, ccnt, o, d, tmax, bt, bk);
@@ -505,6 +555,7 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
             }
             lim = __uint_as_float(group_min32<4>(__float_as_uint(lim)));
         }
+#endif
         if (!done) {
             const bool inner = ccnt == 0 && e <= lim;   // interior child still overlapping [0, lim]
             const uint32_t nkey = inner ? ((__float_as_uint(e) & ~3u) | (uint32_t)c) : ~0u;
