@@ -28,15 +28,8 @@ __device__ __forceinline__ v3 operator+(v3 a, v3 b) { return mk(a.x + b.x, a.y +
 __device__ __forceinline__ v3 operator-(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ v3 operator*(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ v3 operator*(v3 a, float k) { return mk(a.x * k, a.y * k, a.z * k); }
-#ifdef XRT_EXP_FASTDIV   // cost-map experiment builds only (tools/costmap.sh): NOT exact
-__device__ __forceinline__ v3 operator/(v3 a, float k) { const float r = __builtin_amdgcn_rcpf(k); return mk(a.x * r, a.y * r, a.z * r); }
-__device__ __forceinline__ v3 operator/(v3 a, v3 b) {
-    return mk(a.x * __builtin_amdgcn_rcpf(b.x), a.y * __builtin_amdgcn_rcpf(b.y), a.z * __builtin_amdgcn_rcpf(b.z));
-}
-#else
 __device__ __forceinline__ v3 operator/(v3 a, float k) { return mk(a.x / k, a.y / k, a.z / k); }
 __device__ __forceinline__ v3 operator/(v3 a, v3 b) { return mk(a.x / b.x, a.y / b.y, a.z / b.z); }
-#endif
 __device__ __forceinline__ v3 operator-(v3 a) { return mk(-a.x, -a.y, -a.z); }
 // Src/geometry.h:250-261
 __device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
@@ -44,16 +37,8 @@ __device__ __forceinline__ v3 cross(v3 a, v3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 // Src/geometry.cpp:3-16
-#ifdef XRT_EXP_FASTNORM   // cost-map experiment builds only: NOT exact
-__device__ __forceinline__ float length(v3 a) { return __builtin_amdgcn_sqrtf(dot(a, a)); }
-__device__ __forceinline__ v3 normalize(v3 a) {
-    const float r = __builtin_amdgcn_rsqf(dot(a, a));
-    return mk(a.x * r, a.y * r, a.z * r);
-}
-#else
 __device__ __forceinline__ float length(v3 a) { return __builtin_sqrtf(dot(a, a)); }
 __device__ __forceinline__ v3 normalize(v3 a) { return a / length(a); }
-#endif
 // std::min / std::max(a, b)
 __device__ __forceinline__ float smin(float a, float b) { return (b < a) ? b : a; }
 __device__ __forceinline__ float smax(float a, float b) { return (a < b) ? b : a; }
@@ -160,10 +145,6 @@ __device__ __forceinline__ double sincosf_reduce(double x, int& n) {
 //    x exactly (|y| * 2/pi * 2^23 < 2^22), so the reduced evaluation is the same numbers;
 //  * |y| < 2^-12: sinf returns y, cosf 1.0f.
 __device__ __forceinline__ void glibc_sincosf(float y, float& so, float& co) {
-#ifdef XRT_EXP_FASTTRIG   // cost-map experiment builds only: NOT exact
-    so = __sinf(y), co = __cosf(y);
-    return;
-#endif
     const uint32_t top = abstop12(y);
     if (top >= abstop12(120.0f)) {   // |y| >= 120 or NaN/Inf: outside every sampled domain
         so = __builtin_sinf(y), co = __builtin_cosf(y);

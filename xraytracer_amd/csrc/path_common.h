@@ -17,9 +17,6 @@ constexpr int kSphTile = 1024;   // spheres per LDS tile (16 KiB + 4 KiB)
 
 // ============================================================================ RNG ====
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
-#ifdef XRT_EXP_NOTEMPER   // cost-map experiment builds only: NOT exact
-    return y;
-#endif
     y ^= (y >> 11);
     y ^= (y << 7) & 0x9d2c5680u;
     y ^= (y << 15) & 0xefc60000u;

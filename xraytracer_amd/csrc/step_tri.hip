@@ -216,9 +216,6 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
                                              bool ext, v3 o, v3 d, uint32_t shm, const v3 (&so)[NL + 1],
                                              const v3 (&sd)[NL + 1], const float (&stm)[NL + 1],
                                              unsigned long long& best, uint32_t& occ
-#ifdef XRT_PHASE_CLOCK
-                                             , uint64_t* ph_acc, uint32_t* ph_cnt
-#endif
 ) {
     constexpr int R = 1 + NL;
     W.best[lane] = ~0ull;
@@ -256,9 +253,6 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
         wave_sync();
         const uint32_t c = B.count, first = (uint32_t)B.first, magic = B.magic;
         const uint32_t pairs = tot * c;
-#ifdef XRT_PHASE_CLOCK
-        ph_cnt[0] += (pairs + 63) / 64, ph_cnt[1] += pairs, ph_cnt[2] += 1;
-#endif
         for (uint32_t j0 = 0; j0 < pairs; j0 += 64) {
             const uint32_t j = j0 + (uint32_t)lane;
             if (j < pairs) {
@@ -398,6 +392,15 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const D
 #ifndef XRT_BVH_TOP
 #define XRT_BVH_TOP 64   // breadth-first top nodes of the 4-wide BVH kept in LDS (at most; kStepLds bounds it)
 #endif
+#ifndef XRT_DEEP_STEAL
+#define XRT_DEEP_STEAL 0   // idle quads take stacked subtrees of active rays once the pool is drained
+#endif
+constexpr int kQs = 64;          // quad stack entries (circular; >= kBvh4Stack)
+constexpr int kQsMask = kQs - 1;
+static_assert(kQs >= kBvh4Stack, "quad stacks");
+#ifndef XRT_DEEP_EARLY
+#define XRT_DEEP_EARLY 0   // fetch the likely next node before the leaf tests
+#endif
 #ifndef XRT_DEEP_SPREAD
 #define XRT_DEEP_SPREAD 1   // a node's overlapped leaf triangles dealt over the quad's lanes
 #endif
@@ -448,12 +451,19 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
     constexpr uint64_t kLeads = 0x1111111111111111ull;   // lane 0 of every quad
     const int c = lane & 3;
     SE* qs = stk + (lane >> 2);
+    uint32_t* mbox = reinterpret_cast<uint32_t*>(stk + 16 * kQs);   // steals: (pool entry << 16) | node
+    (void)mbox;
     uint32_t next = 0;   // wave-uniform: first ray not yet taken
     bool active = false, any = false;
-    uint32_t id = 0;
-    int node = 0, sp = 0, bk = -1;
+    uint32_t id = 0, ridx = 0;   // the ray's id and its pool entry
+    (void)ridx;
+    int node = 0, sp = 0, base = 0, bk = -1;   // stack entries [base, sp), circular (kQs)
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0), inv = mk(0, 0, 0);
     float tmax = 0.0f, bt = kINF;
+#if XRT_DEEP_EARLY
+    bool have_next = false;   // nlo / nhi hold child c of `node` (fetched during the last step)
+    f4 nlo = make_float4(0, 0, 0, 0), nhi = nlo;
+#endif
 #ifdef XRT_EXPERIMENTS
     uint32_t niter = 0, nsteps = 0;
 #endif
@@ -463,6 +473,7 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
             if (idle) {
                 const uint32_t idx = next + (uint32_t)__popcll(idle & ((1ull << (lane & ~3)) - 1ull));
                 if (!active && idx < n_deep) {
+                    ridx = idx;
                     const f4 A = ray_o[idx], D = ray_d[idx];
                     id = __float_as_uint(D.w);
                     any = id >= 64u;
@@ -473,12 +484,57 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
                         if (key != ~0ull) bt = __uint_as_float((uint32_t)(key >> 32)), bk = (int)(uint32_t)key;
                     }
                     inv = rcp3(d);
-                    node = 0, sp = 0;
+                    node = 0, sp = 0, base = 0;
                     active = true;
+#if XRT_DEEP_EARLY
+                    have_next = false;
+#endif
                 }
                 next += (uint32_t)__popcll(idle);
             }
         }
+#if XRT_DEEP_STEAL
+        // Work stealing once the pool is drained: an idle quad takes the oldest stacked node of
+        // an active ray (the bottom of its stack: the largest pending subtree) and walks that
+        // subtree for the same ray; every quad working on a ray merges into its records (key
+        // minimum, occlusion or) and prunes with the ray's best key so far.  Which quad tests
+        // a triangle does not change the (t, index) minimum nor the occlusion.
+        if (next >= n_deep) {
+            const uint64_t idle = __ballot(!active) & kLeads;
+            const uint64_t vict = __ballot(active && sp - base >= 1) & kLeads;
+            if (idle && vict) {
+                const uint32_t pairs = min((uint32_t)__popcll(idle), (uint32_t)__popcll(vict));
+                const uint64_t below = (1ull << (lane & ~3)) - 1ull;
+                const bool victim = active && sp - base >= 1 && (uint32_t)__popcll(vict & below) < pairs;
+                if (victim) {
+                    if (c == 0) mbox[__popcll(vict & below)] = (ridx << 16) | (uint32_t)qs[(base & kQsMask) * 16];
+                    ++base;
+                }
+                wave_sync();
+                const uint32_t r = (uint32_t)__popcll(idle & below);
+                if (!active && r < pairs) {
+                    const uint32_t m = mbox[r];
+                    ridx = m >> 16;
+                    const f4 A = ray_o[ridx], D = ray_d[ridx];
+                    id = __float_as_uint(D.w);
+                    any = id >= 64u;
+                    o = xyz(A), d = xyz(D), tmax = A.w;
+                    bt = kINF, bk = -1;
+                    if (!any) {
+                        const unsigned long long key = best[id];
+                        if (key != ~0ull) bt = __uint_as_float((uint32_t)(key >> 32)), bk = (int)(uint32_t)key;
+                    }
+                    inv = rcp3(d);
+                    node = (int)(m & 0xffffu), sp = 0, base = 0;
+                    active = true;
+#if XRT_DEEP_EARLY
+                    have_next = false;
+#endif
+                }
+                wave_sync();   // the mailbox is rewritten next time
+            }
+        }
+#endif
         if (!__ballot(active)) break;
 #ifdef XRT_EXPERIMENTS
         ++niter;
@@ -487,6 +543,11 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
         if (!active) continue;
         // ---- one node: child c on lane c; lim = the quad's best t (closest hits) or tmax
         f4 lo, hi;
+#if XRT_DEEP_EARLY
+        if (have_next) {
+            lo = nlo, hi = nhi;
+        } else
+#endif
         if (node < ntop) {
             lo = top[8 * node + c], hi = top[8 * node + 4 + c];
         } else {
@@ -494,8 +555,30 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
         }
         const int cidx = __float_as_int(lo.w), ccnt = __float_as_int(hi.w);
         float lim = any ? tmax : __uint_as_float(group_min32<4>(__float_as_uint(bt)));   // t >= 0: bits order
+#if XRT_DEEP_STEAL
+        if (!any) {   // other quads' finished subtrees of the same ray
+            const unsigned long long gk = best[id];
+            if (gk != ~0ull) lim = __builtin_fminf(lim, __uint_as_float((uint32_t)(gk >> 32)));
+        }
+#endif
         const float e = ccnt >= 0 ? bvh_enter(lo, hi, o, inv, lim) : __builtin_inff();
         bool done = false;
+#if XRT_DEEP_EARLY
+        // The likely next node — the nearest interior child overlapping [0, lim] before the leaf
+        // tests, else the stack top — is fetched now, so its latency overlaps the leaf loads.
+        // The leaf tests can only shrink lim: if that child still overlaps it is still the
+        // nearest and is taken; if not, no child does and the stack top is taken (unchanged).
+        int tnode = -1;
+        {
+            const bool inner0 = ccnt == 0 && e <= lim;
+            const uint32_t k0 = inner0 ? ((__float_as_uint(e) & ~3u) | (uint32_t)c) : ~0u;
+            const uint32_t m0 = group_min32<4>(k0);
+            if (m0 != ~0u) tnode = (int)group_or32<4>(k0 == m0 ? (uint32_t)cidx : 0u);
+            else if (sp > base) tnode = (int)qs[((sp - 1) & kQsMask) * 16];
+            if (tnode >= ntop) nlo = ldg4(P.bvh4, 8 * (size_t)tnode + c), nhi = ldg4(P.bvh4, 8 * (size_t)tnode + 4 + c);
+            else if (tnode >= 0) nlo = top[8 * tnode + c], nhi = top[8 * tnode + 4 + c];
+        }
+#endif
 #if XRT_DEEP_SPREAD
         // The overlapped leaf children's triangles, dealt round robin over the quad's lanes
         // (triangle j of the concatenated leaves to lane j % 4), so one leaf does not make one
@@ -563,20 +646,27 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
             if (nmin != ~0u) {
                 const bool nearest = nkey == nmin;
                 const uint32_t m4 = (uint32_t)(__ballot(inner && !nearest) >> (lane & ~3)) & 0xfu;
-                if (inner && !nearest) qs[(sp + __popc(m4 & ((1u << c) - 1u))) * 16] = (SE)cidx;
+                if (inner && !nearest) qs[((sp + __popc(m4 & ((1u << c) - 1u))) & kQsMask) * 16] = (SE)cidx;
                 sp += __popc(m4);
                 node = (int)group_or32<4>(nearest ? (uint32_t)cidx : 0u);
-            } else if (sp == 0) {
+            } else if (sp == base) {
                 done = true;
             } else {
-                node = (int)qs[(--sp) * 16];
+                node = (int)qs[((--sp) & kQsMask) * 16];
             }
         }
+#if XRT_DEEP_EARLY
+        have_next = !done && node == tnode;
+#endif
         if (done) {
             if (!any) {   // the quad's closest hit: the smallest (t bits, index) of the lanes
                 const uint64_t key = bk >= 0 ? ((uint64_t)__float_as_uint(bt) << 32) | (uint32_t)bk : ~0ull;
                 const uint64_t kmin = group_min64<4>(key);
+#if XRT_DEEP_STEAL
+                if (c == 0 && kmin != ~0ull) atomicMin(&best[id], kmin);
+#else
                 if (c == 0 && kmin != ~0ull) best[id] = kmin;
+#endif
             }
             active = false;
         }
@@ -670,6 +760,7 @@ __device__ __forceinline__ bool deep_park(MergedWave<NL>& Q, uint32_t& pool_n, i
 // BVH nodes, one MergedWave of trace scratch per wave, one MergedWave of parked rays per
 // wave (deep_park), then 16 quad stacks of bvh4_stack 16-bit entries per wave
 // (use_step_bvh: at most 65,536 nodes).
+constexpr uint32_t kStackWave = 16u * kQs * 2u + 64u;   // a wave's 16 quad stacks (16-bit) + the steal mailbox
 struct BvhStepLayout {
     uint32_t tri, obj, light, top, wave, pool, stack, total;
     int ntop;
@@ -682,14 +773,14 @@ __host__ __device__ inline BvhStepLayout bvh_step_layout(const KParams& P, uint3
     B.top = (B.light + (uint32_t)sizeof(DLight) * (uint32_t)P.n_lights + 15u) & ~15u;
     // as many of the top XRT_BVH_TOP nodes as the rest leaves room for within kStepLds
     const uint32_t pool_bytes = XRT_PARK ? (kBlock / 64) * wave_bytes : 0u;
-    const uint32_t rest = B.top + (kBlock / 64) * wave_bytes + pool_bytes + (kBlock / 64) * 16u * (uint32_t)P.bvh4_stack * 2u;
+    const uint32_t rest = B.top + (kBlock / 64) * wave_bytes + pool_bytes + (kBlock / 64) * kStackWave;
     const int fit = rest < kStepLds ? (int)((kStepLds - rest) / 128u) : 0;
     B.ntop = P.bvh4_nodes < XRT_BVH_TOP ? P.bvh4_nodes : XRT_BVH_TOP;
     B.ntop = B.ntop < fit ? B.ntop : fit;
     B.wave = B.top + 128u * (uint32_t)B.ntop;
     B.pool = B.wave + (kBlock / 64) * wave_bytes;
     B.stack = B.pool + pool_bytes;
-    B.total = B.stack + (kBlock / 64) * 16u * (uint32_t)P.bvh4_stack * 2u;
+    B.total = B.stack + (kBlock / 64) * kStackWave;
     return B;
 }
 
@@ -741,13 +832,7 @@ __global__ __launch_bounds__(kBlock, XRT_2A_WAVES) void k_trace_2a_coop(KParams 
         }
         unsigned long long best;
         uint32_t occ;
-#ifdef XRT_PHASE_CLOCK
-        uint64_t ph_acc[16] = {};
-        uint32_t ph_cnt[3] = {};
-        merged_trace<NL>(SO, L, W, lane, want, o, d, smask, so, sd, stm, best, occ, ph_acc, ph_cnt);
-#else
         merged_trace<NL>(SO, L, W, lane, want, o, d, smask, so, sd, stm, best, occ);
-#endif
         float bt = kINF, bu = 0.0f, bv = 0.0f;
         int bk = -1;
         if (want && best != ~0ull) {
@@ -795,22 +880,6 @@ hipError_t launch_trace_2a_coop(const KParams& P, const uint32_t* list, const ui
 // current one twists, and the slot state is not touched — the merged kernel clears
 // ST_RNGREQ when it next loads the slot, which is always after this kernel (one refill
 // launch follows every step launch).
-#ifdef XRT_PHASE_CLOCK
-#define PH_TARGS , ph_acc, ph_cnt
-#define MPH_DECL uint64_t ph_t = __builtin_amdgcn_s_memtime();
-#define MPH_MARK(i)                                          \
-    do {                                                     \
-        const uint64_t ph_n = __builtin_amdgcn_s_memtime();  \
-        ph_acc[i] += ph_n - ph_t;                            \
-        ph_t = ph_n;                                         \
-    } while (0)
-#else
-#define PH_TARGS
-#define MPH_DECL
-#define MPH_MARK(i) \
-    do {            \
-    } while (0)
-#endif
 
 #ifndef XRT_STEP_WAVES
 #define XRT_STEP_WAVES 4
@@ -859,7 +928,7 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
         ntop = Bl.ntop;
         Wp = reinterpret_cast<MergedWave<NL>*>(lb + Bl.wave);
         Qp = reinterpret_cast<MergedWave<NL>*>(lb + Bl.pool);
-        stk = reinterpret_cast<uint16_t*>(lb + Bl.stack) + (tid >> 6) * 16 * P.bvh4_stack;
+        stk = reinterpret_cast<uint16_t*>(lb + Bl.stack + (tid >> 6) * kStackWave);
         lds_copy(const_cast<f4*>(L.tri), P.stri, 3 * P.n_stri, tid);
         lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
         lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid);
@@ -911,11 +980,6 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
         }
     };
     __syncthreads();
-#ifdef XRT_PHASE_CLOCK
-    uint64_t ph_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t ph_vis = 0, ph_cnt[3] = {0, 0, 0};
-    const uint64_t kt0 = __builtin_amdgcn_s_memtime();
-#endif
     zero_parts(P, zero_count);
     const PartIter it = part_iter(P, count, (kBlock / 64) * SPW);
     const uint32_t spp = P.spp, max_depth = P.max_depth, width = P.width;
@@ -977,19 +1041,10 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
             if (k >= spp) st = ST_DONE;
         };
         // jitter draws + PinholeCamera::sampleRay for the next sample (Src/renderer.cpp:44-50)
-#ifdef XRT_EXP_CHEAPSTART   // cost-map experiment builds only: the pixel-centre ray, NOT exact
-        v3 o_c, d_c;
-        camera_ray(P, div_w(P, (float)(int)col + 0.5f), div_h(P, (float)(int)row + 0.5f), o_c, d_c);
-#endif
         auto start_sample = [&]() {
-#ifdef XRT_EXP_CHEAPSTART
-            (void)rng.next(), (void)rng.next();
-            o = o_c, d = d_c;
-#else
             const float u = div_w(P, (float)(int)col + rng.next());
             const float v = div_h(P, (float)(int)row + rng.next());
             camera_ray(P, u, v, o, d);
-#endif
             thr = mk(1, 1, 1), rad = mk(0, 0, 0);
             depth = 0;
             ext = true;
@@ -1030,7 +1085,6 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
             start_sample();
         }
         __builtin_amdgcn_s_waitcnt(0);   // prologue loads done: the loop waits only on its own prefetches
-        MPH_DECL
         bool parked = false, p_ext = false, pf_pending = false;   // BVH: parked slot; its ext_now; words in pf[]
         uint32_t pool_n = 0;                                      // BVH: rays in the pool (wave-uniform)
         for (uint32_t vis = 0; vis < visits; ++vis) {
@@ -1038,15 +1092,14 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
             if (!__ballot(act || shm || parked)) break;
             bool ext_now = act && ext;
             bool proceed = true;   // this lane's trace is complete: shade it this visit
-            MPH_MARK(0);
             unsigned long long best;
             uint32_t occ;
             if constexpr (BVH && !XRT_PARK) {
-                merged_trace<NL, true>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ PH_TARGS);
+                merged_trace<NL, true>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
                 deep_pass<NL, uint16_t>(P, top, ntop, stk, W, lane, root, ext_now, o, d, shm, so, sd, stm, best, occ);
             } else if constexpr (BVH) {
                 ext_now = ext_now && !parked;
-                merged_trace<NL, true>(SO, L, W, lane, ext_now, o, d, parked ? 0u : shm, so, sd, stm, best, occ PH_TARGS);
+                merged_trace<NL, true>(SO, L, W, lane, ext_now, o, d, parked ? 0u : shm, so, sd, stm, best, occ);
                 // a parked lane traced nothing this visit and passes no rays
                 const bool now = deep_park<NL>(Qp[tid >> 6], pool_n, lane, root, ext_now, o, d, parked ? 0u : shm, so,
                                                sd, stm, best, occ);
@@ -1068,15 +1121,13 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
                     wave_sync();   // the pool is refilled from the next visit on
                 }
             } else if constexpr (!LANE) {
-                merged_trace<NL>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ PH_TARGS);
+                merged_trace<NL>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
             } else {
                 group_trace<NL, G>(P.n_objs, L, lplane, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
             }
-            MPH_MARK(1);
             if (!proceed) continue;   // BVH: parked until the pool is walked
             resolve(occ);
             if (BVH ? pf_pending : vis > 0) rng.take();   // the words prefetched at the end of the previous segment
-            MPH_MARK(2);
             if (ext_now) {
                 ++nseg;
                 int hk = -1, obj = -1;
@@ -1090,7 +1141,6 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
                 v3 pos = mk(0, 0, 0), ng = mk(0, 0, 0);
                 if (hk >= 0) pos = ray_at(o, d, ht), ng = tri_ng_at(hk);
                 bool ended = false, alive = false;
-                MPH_MARK(8);
                 if (INTEG == XRT_INTEGRATOR_DIRECT) {
                     // DirectIntegrator::integrate (Src/integrator.h:82-119)
                     if (obj < 0) {
@@ -1121,7 +1171,6 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
                         }
                     }
                 }
-                MPH_MARK(9);
                 if (alive) {
                     // next-event estimation: light samples now, shadow rays traced with the
                     // next trace of the wave
@@ -1152,7 +1201,6 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
                             }
                         }
                     }
-                    MPH_MARK(10);
                     if (INTEG == XRT_INTEGRATOR_DIRECT) {
                         ended = true;
                     } else {
@@ -1178,7 +1226,6 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
                         if (depth >= max_depth) ended = true;
                     }
                 }
-                MPH_MARK(11);
                 if (ended) {
                     ext = false;
                     if (shm) {
@@ -1190,29 +1237,23 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
                     if (kst < spp) start_sample();
                 }
             }
-            MPH_MARK(3);
             rng.prefetch(ring);   // unconditional; first read by take() after the next trace
             pf_pending = true;
-#ifdef XRT_PHASE_CLOCK
-            ++ph_vis;
-#endif
-            MPH_MARK(4);
         }
         // drain: trace the shadow rays still in flight, so no NEE state crosses launches
         if (__ballot(shm != 0)) {
             unsigned long long best;
             uint32_t occ;
             if constexpr (BVH) {
-                merged_trace<NL, true>(SO, L, W, lane, false, o, d, shm, so, sd, stm, best, occ PH_TARGS);
+                merged_trace<NL, true>(SO, L, W, lane, false, o, d, shm, so, sd, stm, best, occ);
                 deep_pass<NL, uint16_t>(P, top, ntop, stk, W, lane, root, false, o, d, shm, so, sd, stm, best, occ);
             } else if constexpr (!LANE) {
-                merged_trace<NL>(SO, L, W, lane, false, o, d, shm, so, sd, stm, best, occ PH_TARGS);
+                merged_trace<NL>(SO, L, W, lane, false, o, d, shm, so, sd, stm, best, occ);
             } else {
                 group_trace<NL, G>(P.n_objs, L, lplane, lane, false, o, d, shm, so, sd, stm, best, occ);
             }
             resolve(occ);
         }
-        MPH_MARK(5);
         bool want_req = false;
         if (live && lead) {
             px[0] = acc.x, px[1] = acc.y, px[2] = acc.z;
@@ -1234,17 +1275,6 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
         wave_append(live && lead && !(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
         wave_refill(P, want_req, s, g, lane, reinterpret_cast<uint32_t*>(&W));
     }
-#ifdef XRT_PHASE_CLOCK
-    if (lane == 0) {
-        for (int q = 0; q < 8; ++q) atomicAdd(P.stats + 8 + q, (unsigned long long)ph_acc[q]);
-        for (int q = 8; q < 16; ++q) atomicAdd(P.stats + 16 + q, (unsigned long long)ph_acc[q]);
-        atomicAdd(P.stats + 16, (unsigned long long)(__builtin_amdgcn_s_memtime() - kt0));
-        atomicAdd(P.stats + 20, (unsigned long long)ph_vis);
-        atomicAdd(P.stats + 21, (unsigned long long)ph_cnt[0]);
-        atomicAdd(P.stats + 22, (unsigned long long)ph_cnt[1]);
-        atomicAdd(P.stats + 23, (unsigned long long)ph_cnt[2]);
-    }
-#endif
 }
 
 // CLEAR: also clear the slot's ST_RNGREQ (the wavefront / k_step schedules, whose kernels

@@ -1488,49 +1488,6 @@ __global__ __launch_bounds__(kBlock, XRT_SHADE_WAVES) void k_shade(KParams P, co
     (void)req_count;
 }
 
-// Debug instrumentation (-DXRT_COUNT_TESTS, experiment builds only): triangle tests done
-// per lane and per wave (a wave pays for an object when any of its lanes needs it).
-#ifdef XRT_COUNT_TESTS
-#define CNT_PARAM , uint32_t &cnt_l, uint32_t &cnt_w
-#define CNT_ARG , cnt_l, cnt_w
-#define CNT_OBJ(ne, n)                   \
-    do {                                 \
-        if (ne) cnt_l += (n);            \
-        if (__ballot(ne)) cnt_w += (n);  \
-    } while (0)
-#else
-#define CNT_PARAM
-#define CNT_ARG
-#define CNT_OBJ(ne, n) \
-    do {               \
-    } while (0)
-#endif
-
-// Debug instrumentation (-DXRT_PHASE_CLOCK, experiment builds only): s_memtime cycles per
-// k_step_tri phase, summed over waves (lane 0) into stats[8 + phase].
-#ifdef XRT_PHASE_CLOCK
-#define PH_DECL uint64_t ph_t = __builtin_amdgcn_s_memtime(); uint64_t ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define PH_MARK(i)                                            \
-    do {                                                      \
-        const uint64_t ph_n = __builtin_amdgcn_s_memtime();   \
-        ph_acc[i] += ph_n - ph_t;                             \
-        ph_t = ph_n;                                          \
-    } while (0)
-#define PH_FLUSH                                                                     \
-    do {                                                                             \
-        if (lane == 0)                                                               \
-            for (int q = 0; q < 8; ++q) atomicAdd(P.stats + 8 + q, (unsigned long long)ph_acc[q]); \
-    } while (0)
-#else
-#define PH_DECL
-#define PH_MARK(i) \
-    do {           \
-    } while (0)
-#define PH_FLUSH \
-    do {         \
-    } while (0)
-#endif
-
 struct HitRec {
     float t, u, v;
     int code;           // winner: (kind << 28) | index, -1 miss
@@ -1579,7 +1536,7 @@ __device__ __forceinline__ bool sphere_bvh(const LScene& L, v3 o, v3 d, float tm
 
 // Scene::intersect over the LDS scene (Src/scene.cpp:190-200)
 template <int SCN>
-__device__ __forceinline__ void closest_l(const KParams& P, const LScene& L, v3 o, v3 d, HitRec& h CNT_PARAM) {
+__device__ __forceinline__ void closest_l(const KParams& P, const LScene& L, v3 o, v3 d, HitRec& h) {
     h.t = kINF, h.u = h.v = 0.0f, h.code = -1, h.surf = -1, h.dp = -1, h.t1 = kINF;
     h.st = h.su = h.sv = h.du = h.dv = 0.0f;
     if (SCN == SCN_TRI) {
@@ -1587,7 +1544,6 @@ __device__ __forceinline__ void closest_l(const KParams& P, const LScene& L, v3 
         for (int ob = 0; ob < P.n_objs; ++ob) {
             const DObjBox B = L.box[ob];
             const bool ne = box_overlap(o, inv, B, h.t);
-            CNT_OBJ(ne, B.count_occ & 0x7fffffff);
             if (!ne) continue;
             const int end = B.first + (B.count_occ & 0x7fffffff);
             for (int k = B.first; k < end; ++k) {
@@ -1641,13 +1597,12 @@ __device__ __forceinline__ void closest_l(const KParams& P, const LScene& L, v3 
 
 // Scene::occluded over the LDS scene (Src/scene.cpp:202-211): area-light objects skipped
 template <int SCN>
-__device__ __forceinline__ bool occluded_l(const KParams& P, const LScene& L, v3 o, v3 d, float tmax CNT_PARAM) {
+__device__ __forceinline__ bool occluded_l(const KParams& P, const LScene& L, v3 o, v3 d, float tmax) {
     if (SCN == SCN_TRI) {
         const v3 inv = rcp3(d);
         for (int ob = 0; ob < P.n_objs; ++ob) {
             const DObjBox B = L.box[ob];
             const bool ne = B.count_occ < 0 && box_overlap(o, inv, B, tmax);
-            CNT_OBJ(ne, B.count_occ & 0x7fffffff);
             if (!ne) continue;
             const int end = B.first + (B.count_occ & 0x7fffffff);
             for (int k = B.first; k < end; ++k) {
@@ -1744,12 +1699,7 @@ __device__ int nee_medium(const KParams& P, const LScene& L, uint32_t s, v3 pos,
     if (!(pdf_dir > 0.0f)) return 0;
     ++nsh;
     HitRec h;
-#ifdef XRT_COUNT_TESTS
-    uint32_t cl = 0, cw = 0;
-    closest_l<SCN>(P, L, pos, wl, h, cl, cw);
-#else
     closest_l<SCN>(P, L, pos, wl, h);
-#endif
     v3 tr = mk(1, 1, 1);
     const float f = hg_eval(P.medium.g, wo, wl);
     if (h.code >= 0) {
@@ -1848,9 +1798,6 @@ __global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, con
         const uint32_t s = i < it.n ? list[it.p * P.part_cap + i] : 0;
         uint32_t st = i < it.n ? P.state[s] : ST_DONE;
         bool want_req = false;
-#ifdef XRT_COUNT_TESTS
-        uint32_t cnt_l = 0, cnt_w = 0;
-#endif
         if (!(st & ST_DONE)) {
         const uint32_t g = P.rng_g[s];
         Rng rng{P.ring + (size_t)s * kRing, P.rng_c[s]};
@@ -1911,7 +1858,7 @@ __global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, con
             if (trace) {
                 ++nseg;
                 HitRec h;
-                closest_l<SCN>(P, L, o, d, h CNT_ARG);
+                closest_l<SCN>(P, L, o, d, h);
                 Surf S;
                 const int obj = surface_l<SCN>(L, o, d, h, S);
                 if (INTEG == XRT_INTEGRATOR_DIRECT) {
@@ -1929,7 +1876,7 @@ __global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, con
                             if (pdf == 0.0f) continue;
                             const float bias = 0.01f;
                             ++nsh;
-                            const bool vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias CNT_ARG);
+                            const bool vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias);
                             const float cosv = smax(0.0f, dot(S.ng, wi));
                             const v3 fr = eval_bxdf(ob);
                             rad = rad + div3s(((fr * (float)vis) * Lv) * cosv, pdf);
@@ -2001,7 +1948,7 @@ __global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, con
                                 if (pdf == 0.0f) continue;
                                 const float bias = 0.01f;
                                 ++nsh;
-                                const bool vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias CNT_ARG);
+                                const bool vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias);
                                 const float cosv = smax(0.0f, dot(S.ng, wi));
                                 const v3 fr = eval_bxdf(ob);
                                 L_light = L_light + (((fr * (float)vis) * Lv) * cosv) / pdf;
@@ -2104,16 +2051,6 @@ __global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, con
         if (nrej) P.c_rej[s] += nrej;
         if (nstall) P.c_stall[s] += nstall;
         }
-#ifdef XRT_COUNT_TESTS
-        {
-            unsigned long long a = cnt_l, b = cnt_w;   // b: per-lane view of the wave's cost
-            for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off);
-            b = b > 0 ? b : 0;
-            unsigned long long bm = b;
-            for (int off = 32; off > 0; off >>= 1) bm = max(bm, (unsigned long long)__shfl_down(bm, off));
-            if (lane == 0) atomicAdd(P.stats + 5, a), atomicAdd(P.stats + 6, bm);
-        }
-#endif
         // live list of the next round and refill requests (partitioned, one atomic per wave)
         wave_append(!(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
         wave_append(want_req, s, P.req + it.p * P.part_cap, req_count + it.p, lane);
@@ -2140,22 +2077,9 @@ struct CoopWave {
 constexpr int kCoopMaxObjs = 32;
 constexpr uint32_t kCoopCap = 512;
 
-#ifdef XRT_PHASE_CLOCK
-#define CT_PARAM , uint64_t* g_ct
-#define CT_ARGP , g_ct
-#else
-#define CT_PARAM
-#define CT_ARGP
-#endif
 template <bool SHADOW>
 __device__ __forceinline__ unsigned long long coop_trace(const KParams& P, const LScene& L, CoopWave& W, int lane,
-                                                         bool want, v3 o, v3 d, float tmax CNT_PARAM CT_PARAM) {
-#ifdef XRT_PHASE_CLOCK
-    uint64_t ct = __builtin_amdgcn_s_memtime();
-#define CT_MARK(q) do { const uint64_t cn = __builtin_amdgcn_s_memtime(); g_ct[(SHADOW ? 4 : 0) + q] += cn - ct; ct = cn; } while (0)
-#else
-#define CT_MARK(q) do {} while (0)
-#endif
+                                                         bool want, v3 o, v3 d, float tmax) {
     uint32_t m = 0, n = 0;
     if (want) {
         const v3 inv = rcp3(d);
@@ -2165,10 +2089,6 @@ __device__ __forceinline__ unsigned long long coop_trace(const KParams& P, const
             if (box_overlap(o, inv, B, SHADOW ? tmax : kINF)) m |= 1u << ob, n += B.count_occ & 0x7fffffff;
         }
     }
-#ifdef XRT_COUNT_TESTS
-    cnt_l += n;
-#endif
-    CT_MARK(0);
     uint32_t incl = n;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -2180,10 +2100,6 @@ __device__ __forceinline__ unsigned long long coop_trace(const KParams& P, const
     W.ro[lane] = make_float4(o.x, o.y, o.z, tmax);
     W.rd[lane] = make_float4(d.x, d.y, d.z, 0.0f);
     W.best[lane] = SHADOW ? 0ull : ~0ull;
-    CT_MARK(1);
-#ifdef XRT_COUNT_TESTS
-    cnt_w += (total + 63) / 64 * 64;
-#endif
     for (uint32_t c0 = 0; c0 < total; c0 += kCoopCap) {
         // expand this lane's pairs that fall into the chunk [c0, c0 + kCoopCap)
         if (n && pre < c0 + kCoopCap && pre + n > c0) {
@@ -2199,7 +2115,6 @@ __device__ __forceinline__ unsigned long long coop_trace(const KParams& P, const
             }
         }
         wave_sync();
-        CT_MARK(2);
         const uint32_t cnt = min(kCoopCap, total - c0);
         for (uint32_t j = lane; j < cnt; j += 64) {
             const uint32_t e = W.pair[j];
@@ -2216,15 +2131,13 @@ __device__ __forceinline__ unsigned long long coop_trace(const KParams& P, const
             }
         }
         wave_sync();
-        CT_MARK(3);
     }
-#undef CT_MARK
     return W.best[lane];
 }
 
 __device__ __forceinline__ void coop_closest(const KParams& P, const LScene& L, CoopWave& W, int lane, bool want, v3 o,
-                                             v3 d, HitRec& h CNT_PARAM CT_PARAM) {
-    const unsigned long long b = coop_trace<false>(P, L, W, lane, want, o, d, kINF CNT_ARG CT_ARGP);
+                                             v3 d, HitRec& h) {
+    const unsigned long long b = coop_trace<false>(P, L, W, lane, want, o, d, kINF);
     h.t = kINF, h.u = h.v = 0.0f, h.code = -1, h.surf = -1, h.dp = -1, h.t1 = kINF;
     h.st = h.su = h.sv = h.du = h.dv = 0.0f;
     if (want && b != ~0ull) {
@@ -2262,12 +2175,6 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
     L.light = reinterpret_cast<const DLight*>(lb + Lo.light);
     L.sobj = reinterpret_cast<const int*>(lb + Lo.sobj);
     const int tid = threadIdx.x, lane = tid & 63;
-#ifdef XRT_PHASE_CLOCK
-    const uint64_t kt0 = __builtin_amdgcn_s_memtime(), kr0 = __builtin_amdgcn_s_memrealtime();
-    uint64_t kt1 = 0;
-    uint32_t ph_vis = 0;
-    uint64_t g_ct[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
     CoopWave& W = reinterpret_cast<CoopWave*>(lb + ((Lo.total + 15u) & ~15u))[tid >> 6];
     lds_copy(const_cast<f4*>(L.tri), P.tri, 3 * P.n_tris, tid);
     lds_copy(const_cast<f4*>(L.tng), P.tri_ng, P.n_tris, tid);
@@ -2278,17 +2185,11 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
     __syncthreads();
     zero_parts(P, zero_count);
     const PartIter it = part_iter(P, count, kBlock);
-#ifdef XRT_PHASE_CLOCK
-    kt1 = __builtin_amdgcn_s_memtime();
-#endif
     for (uint32_t base = it.first; base < it.n; base += it.stride) {
         const uint32_t i = base + tid;
         const uint32_t s = i < it.n ? list[it.p * P.part_cap + i] : 0;
         uint32_t st = i < it.n ? P.state[s] : ST_DONE;
         const bool live = !(st & ST_DONE);
-#ifdef XRT_COUNT_TESTS
-        uint32_t cnt_l = 0, cnt_w = 0;
-#endif
         uint32_t g = 0, depth = 0, k = 0;
         Rng rng{P.ring + (size_t)s * kRing, 0};
         v3 thr = mk(1, 1, 1), rad = mk(0, 0, 0), o = mk(0, 0, 0), d = mk(0, 0, 0), acc = mk(0, 0, 0);
@@ -2307,7 +2208,6 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
             rng.prefetch(g - rng.c);
         }
         uint32_t nseg = 0, nsh = 0, nrej = 0;
-        PH_DECL
         for (uint32_t vis = 0; vis < visits; ++vis) {
             const bool act = live && !(st & ST_DONE) && g - rng.c >= kRngVisit;
             if (!__ballot(act)) break;
@@ -2324,9 +2224,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
             if (!one_hit(INTEG) && P.max_depth == 0) ended = act;   // bounce loop never runs
             const bool ext = act && !ended;
             HitRec h;
-            PH_MARK(0);
-            coop_closest(P, L, W, lane, ext, o, d, h CNT_ARG CT_ARGP);
-            PH_MARK(1);
+            coop_closest(P, L, W, lane, ext, o, d, h);
             // SurfaceInfo of a triangle hit: position, face normal; the shading normal (for
             // Le) and the dpdu/dpdv frame (for the BSDF) are rebuilt from (tri, u, v) where used
             Surf S;
@@ -2372,7 +2270,6 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
                     }
                 }
             }
-            PH_MARK(2);
             // next-event estimation: one cooperative shadow trace per light, in light order
             v3 directL = mk(0, 0, 0);
             for (int l = 0; l < P.n_lights; ++l) {
@@ -2381,9 +2278,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
                 if (alive) Lv = light_sample(L.light[l], S.pos, wi, pdf, tmax, rng);
                 const bool sh = alive && pdf != 0.0f;
                 const float bias = 0.01f;
-                PH_MARK(3);
-                const bool occ = coop_trace<true>(P, L, W, lane, sh, S.pos + S.ng * bias, wi, tmax - bias CNT_ARG CT_ARGP) != 0;
-                PH_MARK(4);
+                const bool occ = coop_trace<true>(P, L, W, lane, sh, S.pos + S.ng * bias, wi, tmax - bias) != 0;
                 if (sh) {
                     ++nsh;
                     const float cosv = smax(0.0f, dot(S.ng, wi));
@@ -2397,7 +2292,6 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
                     }
                 }
             }
-            PH_MARK(3);
             if (alive) {
                 if (INTEG == XRT_INTEGRATOR_DIRECT) {
                     ended = true;
@@ -2421,7 +2315,6 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
                     if (depth >= P.max_depth) ended = true;
                 }
             }
-            PH_MARK(5);
             // finish the sample and start the next one (see k_step)
             while (ended) {
                 ended = false;
@@ -2447,14 +2340,8 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
                     depth = 0;
                 }
             }
-            PH_MARK(6);
             if (act) rng.prefetch(g - rng.c);
-            PH_MARK(7);
-#ifdef XRT_PHASE_CLOCK
-            ++ph_vis;
-#endif
         }
-        PH_FLUSH;
         bool want_req = false;
         if (live) {
             px[0] = acc.x, px[1] = acc.y, px[2] = acc.z;
@@ -2474,32 +2361,9 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
             if (nsh) P.c_shadow[s] += nsh;
             if (nrej) P.c_rej[s] += nrej;
         }
-#ifdef XRT_COUNT_TESTS
-        {
-            unsigned long long a = cnt_l, b = cnt_w;
-            for (int off = 32; off > 0; off >>= 1) a += __shfl_down(a, off);
-            if (lane == 0) atomicAdd(P.stats + 5, a), atomicAdd(P.stats + 6, b / 64);
-        }
-#endif
         wave_append(live && !(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
         wave_append(want_req, s, P.req + it.p * P.part_cap, req_count + it.p, lane);
     }
-#ifdef XRT_PHASE_CLOCK
-    if (lane == 0) {
-        atomicAdd(P.stats + 16, (unsigned long long)(__builtin_amdgcn_s_memtime() - kt0));
-        atomicAdd(P.stats + 17, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - kr0));
-        atomicAdd(P.stats + 18, 1ull);
-        atomicAdd(P.stats + 19, (unsigned long long)(kt1 - kt0));
-        if (ph_vis) {
-            const unsigned long long life = __builtin_amdgcn_s_memtime() - kt0;
-            atomicAdd(P.stats + 20, (unsigned long long)ph_vis);
-            atomicMax(P.stats + 21, life);
-            atomicAdd(P.stats + 22, life);
-            atomicAdd(P.stats + 23, 1ull);
-        }
-        for (int q = 0; q < 8; ++q) atomicAdd(P.stats + 24 + q, (unsigned long long)g_ct[q]);
-    }
-#endif
 }
 
 // ================================================================== k_finish ====

@@ -1029,20 +1029,9 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     }
     unsigned long long hs[40] = {0};
     HIPCHK(c, hipMemcpy(hs, P.stats, 40 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    if (hs[5] || hs[6]) std::fprintf(stderr, "[xrt] triangle tests: lane %llu wave %llu\n", hs[5], hs[6]);
-    if (hs[38])   // experiment builds
+    if (hs[38])   // experiment builds (-DXRT_EXPERIMENTS): BVH walk counters
         std::fprintf(stderr, "[xrt] deep rays %llu node steps %llu wave iterations %llu max wave iterations %llu"
-                     " in-wave walks %llu\n", hs[38], hs[39], hs[37], hs[36], hs[8] || hs[9] ? 0ull : hs[35]);
-    if (hs[8] || hs[9]) {   // -DXRT_PHASE_CLOCK experiment builds
-        std::fprintf(stderr, "[xrt] phase cycles (sum over waves):");
-        for (int q = 8; q < 16; ++q) std::fprintf(stderr, " %llu", hs[q]);
-        std::fprintf(stderr, " | kernel memtime %llu realtime %llu waves %llu prologue %llu | visit iters %llu max life %llu busy life %llu busy waves %llu",
-                     hs[16], hs[17], hs[18], hs[19], hs[20], hs[21], hs[22], hs[23]);
-        std::fprintf(stderr, " | coop closest cull/scan/expand/pass %llu %llu %llu %llu shadow %llu %llu %llu %llu",
-                     hs[24], hs[25], hs[26], hs[27], hs[28], hs[29], hs[30], hs[31]);
-        std::fprintf(stderr, " | shade hit/rr/nee/bsdf %llu %llu %llu %llu", hs[32], hs[33], hs[34], hs[35]);
-        std::fprintf(stderr, "\n");
-    }
+                     " in-wave walks %llu\n", hs[38], hs[39], hs[37], hs[36], hs[35]);
     S.segments = hs[0], S.shadow_rays = hs[1], S.draws = hs[2], S.rejected = hs[3], S.stalled = hs[4];
     S.rng_twists = hs[7];
     S.schedule = !fused ? XRT_SCHED_WAVEFRONT
