@@ -383,30 +383,9 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const D
 // index) against a ray: closest hit as the (t, original index) minimum, or any occluder hit
 // below tmax.  The loads of the whole leaf are issued before the first test.  Mesh::
 // rayTriangleIntersect's decisions via ray_tri_nb (two-level scenes are det_bounded).
-#ifndef XRT_PARK
-#define XRT_PARK 0   // experiment: park slots with deep rays and walk the pool in batches (C4 slower: DESIGN.md §3)
-#endif
-#ifndef XRT_PARK_EIGHTHS
-#define XRT_PARK_EIGHTHS 3   // ... once this many eighths of the wave's slots are parked
-#endif
-#ifndef XRT_BVH_TOP
-#define XRT_BVH_TOP 64   // breadth-first top nodes of the 4-wide BVH kept in LDS (at most; kStepLds bounds it)
-#endif
-#ifndef XRT_DEEP_STEAL
-#define XRT_DEEP_STEAL 0   // idle quads take stacked subtrees of active rays once the pool is drained
-#endif
 constexpr int kQs = 64;          // quad stack entries (circular; >= kBvh4Stack)
 constexpr int kQsMask = kQs - 1;
 static_assert(kQs >= kBvh4Stack, "quad stacks");
-#ifndef XRT_DEEP_EARLY
-#define XRT_DEEP_EARLY 0   // fetch the likely next node before the leaf tests
-#endif
-#ifndef XRT_DEEP_SPREAD
-#define XRT_DEEP_SPREAD 1   // a node's overlapped leaf triangles dealt over the quad's lanes
-#endif
-#ifndef XRT_DEEP_LEAF_BATCH
-#define XRT_DEEP_LEAF_BATCH 2   // triangles whose loads are issued together (1, 2 or 4): registers vs latency
-#endif
 template <bool ANY>
 __device__ __forceinline__ bool deep_leaf(const KParams& P, int first, int count, v3 o, v3 d, float tmax, float& bt,
                                           int& bk) {
@@ -791,9 +770,6 @@ __host__ __device__ inline BvhStepLayout bvh_step_layout(const KParams& P, uint3
 // the (t bits << 32 | local index) minimum is the (t, original index) minimum).  The winner's
 // (t, u, v) are recomputed with Mesh::rayTriangleIntersect's ops as the merged kernel does;
 // rays whose segment reaches the BVH root are queued for k_trace_deep.
-#ifndef XRT_2A_WAVES
-#define XRT_2A_WAVES 1
-#endif
 template <int NL>
 __global__ __launch_bounds__(kBlock, XRT_2A_WAVES) void k_trace_2a_coop(KParams P, const StepObjs SO, const uint32_t* __restrict__ list,
                                                           const uint32_t* __restrict__ count, uint32_t* zero_count) {
@@ -881,9 +857,6 @@ hipError_t launch_trace_2a_coop(const KParams& P, const uint32_t* list, const ui
 // ST_RNGREQ when it next loads the slot, which is always after this kernel (one refill
 // launch follows every step launch).
 
-#ifndef XRT_STEP_WAVES
-#define XRT_STEP_WAVES 4
-#endif
 
 // SPW: path slots per wave (64, 32 or 16), G: lanes per slot (1, or 64 / SPW for the group
 // trace).  With G = 1 and SPW < 64, lanes >= SPW own no slot but take part in every pair
@@ -896,9 +869,6 @@ hipError_t launch_trace_2a_coop(const KParams& P, const uint32_t* list, const ui
 // by merged_trace with original-index keys, the rest by the wave's BVH walk over the parked
 // slots' rays (deep_park); the hit triangle's shading data from global memory.  Same path
 // code otherwise.
-#ifndef XRT_BVH_WAVES
-#define XRT_BVH_WAVES 3   // 3 waves per SIMD (<= 168 VGPRs, no spills with two-triangle leaf batches)
-#endif
 
 template <int INTEG, int NL, int SPW, int G, bool LANE, bool BVH>
 __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void k_step_merged(

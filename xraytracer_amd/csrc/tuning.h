@@ -1,0 +1,81 @@
+// tuning.h — every compile-time knob of the kernels, with its shipped default and the
+// measurement behind it.  Experiment builds override them with -D
+// (csrc/Makefile `variant`, tools/ab.sh); none of them changes a result — only the launch
+// geometry, occupancy and schedule.  Included by wavefront.h, so every source sees one set.
+#pragma once
+
+// ---- live lists
+#ifndef XRT_MAX_PARTS
+#define XRT_MAX_PARTS 1024   // live-list partitions at most (per-segment schedules; C3/C4/C5 -8%..-20% vs 64)
+#endif
+#ifndef XRT_PART_MIN
+#define XRT_PART_MIN 512     // ... of at least this many slots each (the merged schedules: 2048, at most 256)
+#endif
+
+// ---- merged schedules (k_step_merged): slots-per-wave layout by live slots (C2)
+#ifndef XRT_LIVE32
+#define XRT_LIVE32 90000     // below: 16 slots per wave (4 lanes each), above: 32
+#endif
+#ifndef XRT_LIVE16
+#define XRT_LIVE16 20000     // below: 4 slots per wave (16 lanes each; group traces only)
+#endif
+#ifndef XRT_STEP_WAVES
+#define XRT_STEP_WAVES 4     // min waves per SIMD of k_step_merged / k_step (<= 128 VGPRs; 3 or 5: C2 -5% / -9%)
+#endif
+#ifndef XRT_KSTEP_WAVES
+#define XRT_KSTEP_WAVES XRT_STEP_WAVES   // k_step (C3, C5) alone
+#endif
+
+// ---- the fused two-level schedule (k_step_merged<..., BVH = true>: C4)
+#ifndef XRT_BVH_WAVES
+#define XRT_BVH_WAVES 3      // 3 waves per SIMD (<= 168 VGPRs, no spills); 2: C4 -40%, 4: spills
+#endif
+#ifndef XRT_BVH_TOP
+#define XRT_BVH_TOP 64       // top 4-wide BVH nodes kept in LDS (at most; kStepLds bounds it); 192: neutral
+#endif
+#ifndef XRT_DEEP_LEAF_BATCH
+#define XRT_DEEP_LEAF_BATCH 2  // leaf triangles whose loads are issued together (registers vs latency)
+#endif
+#ifndef XRT_DEEP_SPREAD
+#define XRT_DEEP_SPREAD 1    // a node's overlapped leaf triangles dealt over the quad's lanes (C4 -12%)
+#endif
+#ifndef XRT_DEEP_EARLY
+#define XRT_DEEP_EARLY 0     // fetch the likely next node before the leaf tests
+#endif
+#ifndef XRT_DEEP_STEAL
+#define XRT_DEEP_STEAL 0     // idle quads take stacked subtrees of active rays once the wave's rays are all taken
+#endif
+#ifndef XRT_PARK
+#define XRT_PARK 0           // park slots with deep rays and walk the pool in batches (C4 +40..+100%: not kept)
+#endif
+#ifndef XRT_PARK_EIGHTHS
+#define XRT_PARK_EIGHTHS 3   // ... once this many eighths of the wave's slots are parked
+#endif
+
+// ---- wavefront schedule (k_shade / k_trace*, XRT_FLAG_WAVEFRONT)
+#ifndef XRT_SHADE_WAVES
+#define XRT_SHADE_WAVES 1    // k_shade launch bounds (131 VGPRs, 3 waves; forcing 4/5: neutral / +9%)
+#endif
+#ifndef XRT_DEEP_WAVES
+#define XRT_DEEP_WAVES 1     // k_trace_deep4(q) launch bounds (6 or 8 waves spill: -9% / -27%)
+#endif
+#ifndef XRT_2A_WAVES
+#define XRT_2A_WAVES 1       // k_trace_2a_coop launch bounds
+#endif
+
+// ---- volumetric k_step (C5)
+#ifndef XRT_VPT_EVENTS
+#define XRT_VPT_EVENTS 1     // one event (a trace or one collision) per loop iteration
+#endif
+#ifndef XRT_VPT_EV_VISITS
+#define XRT_VPT_EV_VISITS 128  // ... events per slot per launch
+#endif
+#ifndef XRT_VPT_EV_DRAWS
+#define XRT_VPT_EV_DRAWS 4   // ... draws of an event for the refill threshold (a collision draws <= 5)
+#endif
+#ifndef XRT_VPT_EV_PF
+#define XRT_VPT_EV_PF 4      // ... reload the 8-word RNG window below this many words
+#endif
+#ifndef XRT_CORNER_GRID
+#define XRT_CORNER_GRID 1    // dense media also uploaded per cell (8 corners, 32 B): C5 +4%
+#endif

@@ -15,6 +15,7 @@
 #pragma once
 #include <stdint.h>
 
+#include "tuning.h"
 #include "xrt.h"
 
 #ifndef __HIPCC__
@@ -30,39 +31,15 @@ constexpr uint32_t kRngMin = 64;     // request a refill when fewer words than t
 constexpr uint32_t kRngVisit = 16;   // a slot visit needs at least this many (max draws of a
                                      // GI/Direct visit with kMaxLights lights is 13; VPT walks
                                      // suspend themselves below 8)
-#ifndef XRT_MAX_PARTS
-#define XRT_MAX_PARTS 1024
-#endif
-#ifndef XRT_PART_MIN
-#define XRT_PART_MIN 512
-#endif
 constexpr uint32_t kMaxParts = XRT_MAX_PARTS;   // live-list partitions (counters per list)
 constexpr uint32_t kPartMinSlots = XRT_PART_MIN;   // ... of at least this many slots each
 constexpr uint32_t kStepVisits = 32; // fused schedule: path segments per slot per k_step
 constexpr uint32_t kMergedVisits = 64; // merged-trace schedule: segments per slot per launch (at most;
                                        // clamped so a launch's draws fit one refill block)
 constexpr uint32_t kMergedLive64 = 160000;  // merged-trace schedule: live slots for 64 slots per wave
-#ifndef XRT_LIVE32
-#define XRT_LIVE32 90000
-#endif
 constexpr uint32_t kMergedLive32 = XRT_LIVE32;   // ... and for 32 (below: 16 slots, 4 lanes each)
-#ifndef XRT_LIVE16
-#define XRT_LIVE16 20000
-#endif
 constexpr uint32_t kMergedLive16 = XRT_LIVE16;   // ... and for 16 (below: 4 slots, 16 lanes each)
-#ifndef XRT_VPT_EVENTS
-#define XRT_VPT_EVENTS 1
-#endif
 constexpr bool kVptEvents = XRT_VPT_EVENTS != 0;   // VPT k_step: one event (trace or collision) per iteration
-#ifndef XRT_VPT_EV_VISITS
-#define XRT_VPT_EV_VISITS 128
-#endif
-#ifndef XRT_VPT_EV_DRAWS
-#define XRT_VPT_EV_DRAWS 4
-#endif
-#ifndef XRT_VPT_EV_PF
-#define XRT_VPT_EV_PF 4
-#endif
 constexpr uint32_t kVptEventVisits = XRT_VPT_EV_VISITS;   // ... events per slot per launch
 constexpr uint32_t kVptEventDraws = XRT_VPT_EV_DRAWS;     // ... draws of an event for the refill threshold (a
                                            // collision draws <= 5; a lane with fewer words left stops early)

@@ -20,12 +20,6 @@
 
 // minimum waves per SIMD the wavefront kernels are compiled for (launch bounds; experiment
 // builds override them)
-#ifndef XRT_SHADE_WAVES
-#define XRT_SHADE_WAVES 1
-#endif
-#ifndef XRT_DEEP_WAVES
-#define XRT_DEEP_WAVES 1
-#endif
 
 namespace xrt {
 
@@ -1743,12 +1737,6 @@ __device__ int nee_resume(const KParams& P, uint32_t s, v3 thr_m, v3& rad, Rng& 
     return 0;
 }
 
-#ifndef XRT_STEP_WAVES
-#define XRT_STEP_WAVES 4   // min waves per SIMD the compiler must fit k_step into (<= 128 VGPRs)
-#endif
-#ifndef XRT_KSTEP_WAVES
-#define XRT_KSTEP_WAVES XRT_STEP_WAVES
-#endif
 template <int SCN, int INTEG>
 __global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, const uint32_t* __restrict__ list,
                                                   const uint32_t* __restrict__ count, uint32_t* __restrict__ out,

@@ -620,9 +620,6 @@ static int set_medium_one(xrt_ctx* c, const xrt_medium_desc* m) {
     DMedium& D = c->base.medium;
     D = DMedium{};
     D.density = as<float>(c->density);
-#ifndef XRT_CORNER_GRID
-#define XRT_CORNER_GRID 1
-#endif
     // the per-cell corner layout (8x the grid's bytes; skipped above 2 GiB).  It is only an
     // acceleration: when the host copy or the device buffer cannot be had, the medium reads
     // the dense grid's rows instead (D.corners = null), with identical results.
