@@ -139,8 +139,9 @@ def hip_kernel_name(kid, sched, scene):
     rocprofv3 reports, which the PMC summaries are keyed by)."""
     from xraytracer_amd import abi
     if kid == abi.XRT_K_STEP:
-        return "k_" + abi.SCHEDULE_NAMES[sched] if sched in (abi.XRT_SCHED_STEP_TRI, abi.XRT_SCHED_STEP_MERGED) \
-            else "k_step"
+        if sched in (abi.XRT_SCHED_STEP_MERGED, abi.XRT_SCHED_STEP_BVH):   # k_step_merged<..., BVH>
+            return "k_step_merged"
+        return "k_step_tri" if sched == abi.XRT_SCHED_STEP_TRI else "k_step"
     if kid == abi.XRT_K_TRACE and scene.desc.n_tris > 1024:   # two-level trace: phase A
         return "k_trace_2a_coop"
     return "k_" + abi.KERNEL_NAMES[kid]

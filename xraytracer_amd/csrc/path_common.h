@@ -644,7 +644,7 @@ __device__ __forceinline__ void lds_copy(T* dst, const T* src, int n, int tid) {
     const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
     uint32_t* d = reinterpret_cast<uint32_t*>(dst);
     const int words = n * (int)(sizeof(T) / 4);
-    for (int q = tid; q < words; q += kBlock) d[q] = s[q];
+    for (int q = tid; q < words; q += (int)blockDim.x) d[q] = s[q];
 }
 
 

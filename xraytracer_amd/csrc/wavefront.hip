@@ -1737,8 +1737,8 @@ __device__ int nee_resume(const KParams& P, uint32_t s, v3 thr_m, v3& rad, Rng& 
     return 0;
 }
 
-template <int SCN, int INTEG>
-__global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, const uint32_t* __restrict__ list,
+template <int SCN, int INTEG, int BS = kBlock>
+__global__ __launch_bounds__(BS, XRT_KSTEP_WAVES) void k_step(KParams P, const uint32_t* __restrict__ list,
                                                   const uint32_t* __restrict__ count, uint32_t* __restrict__ out,
                                                   uint32_t* out_count, uint32_t* zero_count, uint32_t* req_count,
                                                   uint32_t visits) {
@@ -1780,7 +1780,7 @@ __global__ __launch_bounds__(kBlock, XRT_KSTEP_WAVES) void k_step(KParams P, con
     __syncthreads();
     zero_parts(P, zero_count);
     const int lane = tid & 63;
-    const PartIter it = part_iter(P, count, kBlock);
+    const PartIter it = part_iter(P, count, BS);
     for (uint32_t base = it.first; base < it.n; base += it.stride) {
         const uint32_t i = base + tid;
         const uint32_t s = i < it.n ? list[it.p * P.part_cap + i] : 0;
@@ -2637,6 +2637,14 @@ static hipError_t step_i(const KParams& P, const uint32_t* list, const uint32_t*
                          uint32_t* out_count, uint32_t* zero, uint32_t* req_count, uint32_t visits, uint32_t blocks,
                          hipStream_t st) {
     const size_t lds = step_lds_bytes(P);
+    // Sphere-BVH scenes (C3) keep ~45 KB of BVH and spheres in LDS, so 256-thread blocks stop
+    // at 3 per CU (3 waves per SIMD); 512-thread blocks share one copy between 8 waves
+    // (4 waves per SIMD, the VGPR limit).  Same partitions, same results.
+    if (SCN == SCN_SPHERE && P.n_snode > 0 && kStepBlock512 && P.integrator == XRT_INTEGRATOR_DIRECT) {
+        hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_DIRECT, 512>), dim3((blocks + 1) / 2), dim3(512), lds, st, P,
+                           list, count, out, out_count, zero, req_count, visits);
+        return hipGetLastError();
+    }
     if (P.integrator == XRT_INTEGRATOR_DIRECT)
         hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_DIRECT>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
                            out, out_count, zero, req_count, visits);
