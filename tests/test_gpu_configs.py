@@ -126,6 +126,31 @@ def test_c3_geometry_across_launches(renderer):
     compare(img[k::n], ref[k::n])
 
 
+def test_c3_row_shard(renderer):
+    """C3 as one rank of 8 renders it (rows y % 8 == 3: 90 x 1280 slots, 224 partitions — a
+    grid that is not a power-of-two multiple of the partitions), 8 spp, zeros elsewhere, rows
+    y % 64 == 3 bit-exact against the oracle."""
+    import torch
+
+    c = scenes.CONFIGS["C3"]
+    w, h, spp = c["width"], c["height"], 8
+    scene = scenes.build("C3")
+    renderer.spp = spp
+    renderer.upload(scene)
+    fb = torch.full((h, w, 3), 7.0, dtype=torch.float32, device="cuda:0")
+    renderer.render_device(scene, w, h, fb.data_ptr(), after_stream=torch.cuda.current_stream().cuda_stream,
+                           timing=True, schedule="auto", shard_index=3, shard_count=8)
+    g = renderer.stats
+    img = fb.cpu().numpy()
+    assert g.schedule == abi.XRT_SCHED_STEP and g.partitions == partitions(90 * 1280) == 224
+    assert g.samples == 90 * 1280 * spp
+    owned = np.zeros(h, bool)
+    owned[3::8] = True
+    assert np.all(img[~owned] == 0)
+    ref, _ = pyoracle.render(scene, w, h, spp, shard_index=3, shard_count=64)
+    compare(img[3::64], ref[3::64])
+
+
 def test_c3_geometry(renderer):
     """C3 (1,000 spheres + sphere light, 1280x720, Direct): fused k_step with the LDS
     skip-link sphere BVH, 1024 partitions."""

@@ -2641,8 +2641,11 @@ static hipError_t step_i(const KParams& P, const uint32_t* list, const uint32_t*
     // at 3 per CU (3 waves per SIMD); 512-thread blocks share one copy between 8 waves
     // (4 waves per SIMD, the VGPR limit).  Same partitions, same results.
     if (SCN == SCN_SPHERE && P.n_snode > 0 && kStepBlock512 && P.integrator == XRT_INTEGRATOR_DIRECT) {
-        hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_DIRECT, 512>), dim3((blocks + 1) / 2), dim3(512), lds, st, P,
-                           list, count, out, out_count, zero, req_count, visits);
+        // the grid must stay a multiple of n_part (part_iter: block b serves partition b % n_part
+        // and chunk b / n_part of gridDim / n_part chunks)
+        const uint32_t chunks = std::max(1u, blocks / P.n_part);
+        hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_DIRECT, 512>), dim3(P.n_part * ((chunks + 1) / 2)), dim3(512),
+                           lds, st, P, list, count, out, out_count, zero, req_count, visits);
         return hipGetLastError();
     }
     if (P.integrator == XRT_INTEGRATOR_DIRECT)
@@ -2676,6 +2679,7 @@ hipError_t launch_step(const KParams& P, const KParams* dP, const uint32_t* list
                        uint32_t* out_count, uint32_t* zero, uint32_t* req_count, uint32_t visits, uint32_t blocks,
                        hipStream_t st) {
     if (!step_lds_bytes(P)) return hipErrorInvalidValue;
+    if (P.n_part == 0 || blocks % P.n_part != 0) return hipErrorInvalidValue;   // part_iter's grid contract
     if (use_step_tri(P)) {
         const size_t lds = ((step_layout(P).total + 15u) & ~15u) + (kBlock / 64) * sizeof(CoopWave);
         if (P.integrator == XRT_INTEGRATOR_DIRECT)
