@@ -390,10 +390,10 @@ template <bool ANY>
 __device__ __forceinline__ bool deep_leaf(const KParams& P, int first, int count, v3 o, v3 d, float tmax, float& bt,
                                           int& bk) {
     constexpr int B = XRT_DEEP_LEAF_BATCH;
-    static_assert(kBvhLeaf % B == 0, "leaf batches");
+    static_assert(kBvhLeafTri % B == 0, "leaf batches");
     bool occ = false;
 #pragma unroll
-    for (int q0 = 0; q0 < (int)kBvhLeaf; q0 += B) {
+    for (int q0 = 0; q0 < (int)kBvhLeafTri; q0 += B) {
         if (q0 >= count) break;
         f4 T[B][3];
 #pragma unroll

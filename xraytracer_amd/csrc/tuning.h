@@ -33,6 +33,9 @@
 #ifndef XRT_BVH_WAVES
 #define XRT_BVH_WAVES 3      // 3 waves per SIMD (<= 168 VGPRs, no spills); 2: C4 -40%, 4: spills
 #endif
+#ifndef XRT_BVH_LEAF
+#define XRT_BVH_LEAF 4       // triangles per leaf of the triangle BVH (at most)
+#endif
 #ifndef XRT_BVH_TOP
 #define XRT_BVH_TOP 64       // top 4-wide BVH nodes kept in LDS (at most; kStepLds bounds it); 192: neutral
 #endif

@@ -119,7 +119,8 @@ struct StepObjs {
     StepObj o[kMergedMaxObjs];
     int n;
 };
-constexpr uint32_t kBvhLeaf = 4;      // BVH: primitives per leaf (at most)
+constexpr uint32_t kBvhLeaf = 4;      // sphere BVH (C3): primitives per leaf (at most)
+constexpr uint32_t kBvhLeafTri = XRT_BVH_LEAF;   // triangle BVH (C4): triangles per leaf (at most)
 constexpr int kBvhMaxDepth = 48;      // BVH build: depth bound (SAH above max - 24 levels, median below)
 constexpr int kBvhStack = 24;         // k_trace_bvh: LDS traversal stack entries per thread (> tree depth)
 constexpr int kBvh4Stack = 48;        // k_trace_deep4: LDS stack entries per lane (>= 3 * 4-wide depth + 1)

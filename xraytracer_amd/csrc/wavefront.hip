@@ -449,13 +449,13 @@ __global__ __launch_bounds__(kBlock) void k_trace_2a(KParams P, const uint32_t* 
 template <bool ANY>
 __device__ __forceinline__ bool bvh_leaf_batch(const KParams& P, int first, int count, v3 o, v3 d, float tmax,
                                                float& bt, float& bu, float& bv, int& bk) {
-    f4 T[kBvhLeaf][3];
+    f4 T[kBvhLeafTri][3];
 #pragma unroll
-    for (int q = 0; q < (int)kBvhLeaf; ++q)
+    for (int q = 0; q < (int)kBvhLeafTri; ++q)
         if (q < count) T[q][0] = P.bvh_tri[3 * (first + q)], T[q][1] = P.bvh_tri[3 * (first + q) + 1],
                        T[q][2] = P.bvh_tri[3 * (first + q) + 2];
 #pragma unroll
-    for (int q = 0; q < (int)kBvhLeaf; ++q) {
+    for (int q = 0; q < (int)kBvhLeafTri; ++q) {
         if (q >= count) break;
         if (ANY && T[q][1].w == 0.0f) continue;   // area-light objects never occlude
         float t, u, v;

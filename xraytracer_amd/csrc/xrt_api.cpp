@@ -524,7 +524,7 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
                 P.sstep = P.det_bounded ? &c->sstep : nullptr;   // k_trace_2a_coop: ray_tri_nb
             }
         }
-        const BvhBuild B = build_bvh(mn.data(), mx.data(), (uint32_t)nt, kBvhLeaf, 1e-4f * diag + 1e-4f, kBvhMaxDepth);
+        const BvhBuild B = build_bvh(mn.data(), mx.data(), (uint32_t)nt, kBvhLeafTri, 1e-4f * diag + 1e-4f, kBvhMaxDepth);
         if (B.depth >= kBvhStack) return set_err(c, XRT_ERR_UNSUPPORTED, "BVH deeper than the traversal stack");
         std::vector<f4> btri(3 * nt);
         for (size_t i = 0; i < nt; ++i) {
