@@ -23,7 +23,7 @@
 #define XRT_STEP_WAVES 4     // min waves per SIMD of k_step_merged / k_step (<= 128 VGPRs; 3 or 5: C2 -5% / -9%)
 #endif
 #ifndef XRT_KSTEP_512
-#define XRT_KSTEP_512 1      // C3's k_step in 512-thread blocks (one LDS copy of the sphere BVH per 8 waves)
+#define XRT_KSTEP_512 0      // C3: k_step in 512-thread blocks (one LDS copy per 8 waves): -2% 1 GPU, -9% 8 shards
 #endif
 #ifndef XRT_KSTEP_WAVES
 #define XRT_KSTEP_WAVES XRT_STEP_WAVES   // k_step (C3, C5) alone
