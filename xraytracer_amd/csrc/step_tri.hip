@@ -1386,6 +1386,10 @@ uint32_t step_merged_spw(const KParams& P, uint64_t live) {
     if (P.spw_req == 4) return group ? 4u : 16u;
     if (P.spw_req == 8) return group ? 8u : 16u;
     if (P.spw_req == 16 || P.spw_req == 32 || P.spw_req == 64) return P.spw_req;
+    // two-level scenes (C4, tools/spw_sweep.sh): fewer slots per wave leave more
+    // quads per deep ray and more lanes per pair pass, which pays once the GPU is not full:
+    // full waves above kBvhLive64 live slots, 32 above kBvhLive32, then 16
+    if (P.two_level) return live >= kBvhLive64 ? 64u : live >= kBvhLive32 ? 32u : 16u;
     // measured on C2 (tools/shard_sim.py): full waves down to ~160k live
     // slots, 32 slots per wave down to ~90k, 16 (4 lanes per slot) down to kMergedLive16,
     // then 4 (16 lanes per slot: the tail of a small shard, where a visit's latency, not

@@ -33,6 +33,12 @@
 #ifndef XRT_BVH_WAVES
 #define XRT_BVH_WAVES 3      // 3 waves per SIMD (<= 168 VGPRs, no spills); 2: C4 -40%, 4: spills
 #endif
+#ifndef XRT_BVH_LIVE64
+#define XRT_BVH_LIVE64 750000   // live slots above which two-level scenes take 64 slots per wave
+#endif
+#ifndef XRT_BVH_LIVE32
+#define XRT_BVH_LIVE32 250000   // ... 32 above this, else 16 (C4 64 spp: 8 shards 21.0 -> 16.6 ms)
+#endif
 #ifndef XRT_BVH_LEAF
 #define XRT_BVH_LEAF 4       // triangles per leaf of the triangle BVH (at most)
 #endif

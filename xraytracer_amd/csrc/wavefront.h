@@ -38,6 +38,8 @@ constexpr uint32_t kMergedVisits = 64; // merged-trace schedule: segments per sl
                                        // clamped so a launch's draws fit one refill block)
 constexpr uint32_t kMergedLive64 = 160000;  // merged-trace schedule: live slots for 64 slots per wave
 constexpr uint32_t kMergedLive32 = XRT_LIVE32;   // ... and for 32 (below: 16 slots, 4 lanes each)
+constexpr uint32_t kBvhLive64 = XRT_BVH_LIVE64;   // two-level merged schedule: 64 slots per wave above this
+constexpr uint32_t kBvhLive32 = XRT_BVH_LIVE32;   // ... 32 above this, else 16
 constexpr uint32_t kMergedLive16 = XRT_LIVE16;   // ... and for 16 (below: 4 slots, 16 lanes each)
 constexpr bool kVptEvents = XRT_VPT_EVENTS != 0;   // VPT k_step: one event (trace or collision) per iteration
 constexpr uint32_t kVptEventVisits = XRT_VPT_EV_VISITS;   // ... events per slot per launch
