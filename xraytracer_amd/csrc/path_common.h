@@ -640,11 +640,11 @@ __device__ __forceinline__ v3 tri_ns_l(const LScene& L, int i, float u, float v)
 
 
 template <typename T>
-__device__ __forceinline__ void lds_copy(T* dst, const T* src, int n, int tid) {
+__device__ __forceinline__ void lds_copy(T* dst, const T* src, int n, int tid, int stride = kBlock) {
     const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
     uint32_t* d = reinterpret_cast<uint32_t*>(dst);
     const int words = n * (int)(sizeof(T) / 4);
-    for (int q = tid; q < words; q += (int)blockDim.x) d[q] = s[q];
+    for (int q = tid; q < words; q += stride) d[q] = s[q];
 }
 
 

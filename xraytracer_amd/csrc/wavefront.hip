@@ -1756,26 +1756,26 @@ __global__ __launch_bounds__(BS, XRT_KSTEP_WAVES) void k_step(KParams P, const u
     L.light = reinterpret_cast<const DLight*>(lb + Lo.light);
     L.sobj = reinterpret_cast<const int*>(lb + Lo.sobj);
     const int tid = threadIdx.x;
-    lds_copy(const_cast<f4*>(L.tri), P.tri, 3 * P.n_tris, tid);
-    lds_copy(const_cast<f4*>(L.tng), P.tri_ng, P.n_tris, tid);
-    lds_copy(const_cast<f4*>(L.nrm), P.tri_nrm, 3 * P.n_tris, tid);
-    if (SCN == SCN_TRI) lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid);
-    lds_copy(const_cast<f4*>(L.bx), P.box, 2 * P.n_box, tid);
-    lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid);
+    lds_copy(const_cast<f4*>(L.tri), P.tri, 3 * P.n_tris, tid, BS);
+    lds_copy(const_cast<f4*>(L.tng), P.tri_ng, P.n_tris, tid, BS);
+    lds_copy(const_cast<f4*>(L.nrm), P.tri_nrm, 3 * P.n_tris, tid, BS);
+    if (SCN == SCN_TRI) lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid, BS);
+    lds_copy(const_cast<f4*>(L.bx), P.box, 2 * P.n_box, tid, BS);
+    lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid, BS);
     if (SCN == SCN_SPHERE && P.n_snode > 0) {
         // sphere BVH in LDS; per-hit tables read from global memory (step_layout)
         L.snode = reinterpret_cast<const f4*>(lb + Lo.snode);
         L.ssph = reinterpret_cast<const f4*>(lb + Lo.ssph);
         L.sbk = reinterpret_cast<const int*>(lb + Lo.sbk);
         L.n_snode = P.n_snode;
-        lds_copy(const_cast<f4*>(L.snode), P.snode, 2 * P.n_snode, tid);
-        lds_copy(const_cast<f4*>(L.ssph), P.ssph, P.n_sph, tid);
-        lds_copy(const_cast<int*>(L.sbk), P.sbk, P.n_sph, tid);
+        lds_copy(const_cast<f4*>(L.snode), P.snode, 2 * P.n_snode, tid, BS);
+        lds_copy(const_cast<f4*>(L.ssph), P.ssph, P.n_sph, tid, BS);
+        lds_copy(const_cast<int*>(L.sbk), P.sbk, P.n_sph, tid, BS);
         L.sph = P.sph, L.sobj = P.sph_obj, L.obj = P.objs;
     } else {
-        lds_copy(const_cast<f4*>(L.sph), P.sph, P.n_sph, tid);
-        lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
-        lds_copy(const_cast<int*>(L.sobj), P.sph_obj, P.n_sph, tid);
+        lds_copy(const_cast<f4*>(L.sph), P.sph, P.n_sph, tid, BS);
+        lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid, BS);
+        lds_copy(const_cast<int*>(L.sobj), P.sph_obj, P.n_sph, tid, BS);
     }
     __syncthreads();
     zero_parts(P, zero_count);
