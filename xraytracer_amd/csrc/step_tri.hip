@@ -520,6 +520,79 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
         nsteps += (uint32_t)__popcll(__ballot(active) & kLeads);
 #endif
         if (!active) continue;
+#if XRT_DEEP_FLAT
+        // ---- one node, with as few divergent branches as the step allows (the loop's exec-mask
+        // bookkeeping cost about as many scalar instructions as it had vector ones): the node
+        // from LDS or global memory through one generic pointer, every leaf triangle's test and
+        // both reductions computed for closest-hit and any-hit rays alike, the stack top read
+        // every step.  Same decisions and results as the branchy form below.
+        const f4* N = node < ntop ? top + 8 * node : P.bvh4 + 8 * (size_t)node;
+        const f4 lo = N[c], hi = N[4 + c];
+        const int cidx = __float_as_int(lo.w), ccnt = __float_as_int(hi.w);
+        const float lim0 = any ? tmax : __uint_as_float(group_min32<4>(__float_as_uint(bt)));   // t >= 0: bits order
+        const float e = ccnt >= 0 ? bvh_enter(lo, hi, o, inv, lim0) : __builtin_inff();
+        bool oc = false;
+        {
+            // the overlapped leaf children's triangles, dealt round robin over the quad's lanes
+            const uint32_t mine = (ccnt > 0 && e != __builtin_inff()) ? (uint32_t)ccnt : 0u;
+            const uint32_t n0 = dpp32<0x00>(mine), n1 = dpp32<0x55>(mine), n2 = dpp32<0xAA>(mine), n3 = dpp32<0xFF>(mine);
+            const uint32_t f0 = dpp32<0x00>((uint32_t)cidx), f1 = dpp32<0x55>((uint32_t)cidx);
+            const uint32_t f2 = dpp32<0xAA>((uint32_t)cidx), f3 = dpp32<0xFF>((uint32_t)cidx);
+            const uint32_t p1 = n0, p2 = n0 + n1, p3 = p2 + n2, tot = p3 + n3;
+            constexpr int B = XRT_DEEP_LEAF_BATCH;
+            for (uint32_t j0 = (uint32_t)c; j0 < tot; j0 += 4u * B) {
+                f4 T[B][3];
+                bool ok[B];
+#pragma unroll
+                for (int b = 0; b < B; ++b) {   // out-of-range slots load triangle 0, unused
+                    const uint32_t j = j0 + 4u * (uint32_t)b;
+                    ok[b] = j < tot;
+                    const uint32_t t = !ok[b] ? 0u : j < p1 ? f0 + j : j < p2 ? f1 + (j - p1) : j < p3 ? f2 + (j - p2)
+                                                                                                          : f3 + (j - p3);
+                    const size_t i = 3 * (size_t)t;
+                    T[b][0] = ldg4(P.bvh_tri, i), T[b][1] = ldg4(P.bvh_tri, i + 1), T[b][2] = ldg4(P.bvh_tri, i + 2);
+                }
+#pragma unroll
+                for (int b = 0; b < B; ++b) {
+                    float t;
+                    const bool hit = ok[b] && ray_tri_nb(o, d, xyz(T[b][0]), xyz(T[b][1]), xyz(T[b][2]), t);
+                    // any hit: area-light objects never occlude (e1.w = occluder flag)
+                    oc |= hit && T[b][1].w != 0.0f && t < tmax;
+                    const int k = __float_as_int(T[b][2].w);
+                    const bool upd = !any && hit && (t < bt || (t == bt && k < bk));
+                    bt = upd ? t : bt;
+                    bk = upd ? k : bk;
+                }
+            }
+        }
+        bool done = any && group_or32<4>(oc ? 1u : 0u) != 0u;
+        if (done && c == 0) atomicOr(&occ[id & 63u], 1u << ((id >> 6) - 1u));
+        const float lim = any ? tmax : __uint_as_float(group_min32<4>(__float_as_uint(__builtin_fminf(lim0, bt))));
+        {
+            const bool inner = !done && ccnt == 0 && e <= lim;   // interior child still overlapping [0, lim]
+            const uint32_t nkey = inner ? ((__float_as_uint(e) & ~3u) | (uint32_t)c) : ~0u;
+            const uint32_t nmin = group_min32<4>(nkey);
+            const bool has = nmin != ~0u;
+            const bool nearest = inner && nkey == nmin;
+            const uint32_t m4 = (uint32_t)(__ballot(inner && !nearest) >> (lane & ~3)) & 0xfu;
+            if (inner && !nearest) qs[((sp + __popc(m4 & ((1u << c) - 1u))) & kQsMask) * 16] = (SE)cidx;
+            sp += __popc(m4);
+            const int child = (int)group_or32<4>(nearest ? (uint32_t)cidx : 0u);
+            const bool pop = !done && !has && sp > base;
+            const int top_entry = (int)qs[((sp - 1) & kQsMask) * 16];   // read every step; used on a pop
+            sp -= pop ? 1 : 0;
+            node = has ? child : top_entry;
+            done = done || (!has && !pop);
+        }
+        if (done) {
+            if (!any) {   // the quad's closest hit: the smallest (t bits, index) of the lanes
+                const uint64_t key = bk >= 0 ? ((uint64_t)__float_as_uint(bt) << 32) | (uint32_t)bk : ~0ull;
+                const uint64_t kmin = group_min64<4>(key);
+                if (c == 0 && kmin != ~0ull) best[id] = kmin;
+            }
+            active = false;
+        }
+#else
         // ---- one node: child c on lane c; lim = the quad's best t (closest hits) or tmax
         f4 lo, hi;
 #if XRT_DEEP_EARLY
@@ -649,6 +722,7 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
             }
             active = false;
         }
+#endif
     }
 #ifdef XRT_EXPERIMENTS
     if (lane == 0) {

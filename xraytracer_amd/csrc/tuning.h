@@ -51,6 +51,9 @@
 #ifndef XRT_DEEP_SPREAD
 #define XRT_DEEP_SPREAD 1    // a node's overlapped leaf triangles dealt over the quad's lanes (C4 -12%)
 #endif
+#ifndef XRT_DEEP_FLAT
+#define XRT_DEEP_FLAT 1      // the walk step with few divergent branches (leaf spread built in; no early / steal)
+#endif
 #ifndef XRT_DEEP_EARLY
 #define XRT_DEEP_EARLY 0     // fetch the likely next node before the leaf tests
 #endif
