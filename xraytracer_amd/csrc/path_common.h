@@ -576,12 +576,11 @@ __device__ __forceinline__ void camera_ray(const KParams& P, float u, float v, v
 // geometric and vertex normals, per-object culling boxes (triangle scenes), spheres,
 // medium boxes, the object and light tables, sphere->object map.
 struct StepLayout {
-    uint32_t tri, tng, nrm, box, sph, bx, obj, light, sobj, snode, ssph, sbk, sbo, uobj, total;
+    uint32_t tri, tng, nrm, box, sph, bx, obj, light, sobj, snode, ssph, sbk, total;
 };
 // Sphere scenes with a skip-link BVH (P.n_snode > 0, C3) keep the BVH, the spheres in leaf
-// order, their index/occluder words and their objects' distinct records (per leaf-order
-// sphere an index into them) in LDS, so a hit's shading reads no global memory; the
-// original-order tables stay in global memory.
+// order and their index/occluder words in LDS; the original-order sphere, sphere-object
+// and object tables (read once per hit, at shading) stay in global memory.
 __host__ __device__ inline StepLayout step_layout(const KParams& P) {
     const bool sb = P.n_snode > 0;
     StepLayout L;
@@ -597,9 +596,7 @@ __host__ __device__ inline StepLayout step_layout(const KParams& P) {
     L.snode = L.sobj + (sb ? 0u : 4u * P.n_sph);
     L.ssph = L.snode + 32u * (uint32_t)P.n_snode;
     L.sbk = L.ssph + (sb ? 16u * P.n_sph : 0u);
-    L.sbo = L.sbk + (sb ? 4u * P.n_sph : 0u);
-    L.uobj = L.sbo + (sb ? 4u * P.n_sph : 0u);
-    L.total = L.uobj + (sb ? (uint32_t)sizeof(DObj) * P.n_uobj : 0u);
+    L.total = L.sbk + (sb ? 4u * P.n_sph : 0u);
     return L;
 }
 
@@ -632,7 +629,6 @@ struct LScene {
     const f4* snode = nullptr;   // sphere BVH (SkipNode: {bmin, skip}, {bmax, leaf}); n_snode > 0
     const f4* ssph = nullptr;    // spheres in BVH leaf order
     const int* sbk = nullptr;    // original sphere index | (occluder << 30)
-    const int* sbo = nullptr;    // per leaf-order sphere: its object's record in obj (= the uobj table)
     int n_snode = 0;
 };
 

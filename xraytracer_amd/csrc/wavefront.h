@@ -201,9 +201,7 @@ struct KParams {
     const f4* snode;          // sphere scenes: threaded BVH (bvh.h SkipNode, 2 f4 each), else null
     const f4* ssph;           // spheres in BVH leaf order (center, radius)
     const int* sbk;           // per ssph entry: original sphere index | (occluder << 30)
-    const int* sbo;           // per ssph entry: its object's record in uobj (the fused k_step's LDS tables)
-    const DObj* uobj;         // the sphere objects' distinct DObj records (C3: two)
-    int n_snode, n_uobj;
+    int n_snode;
     int n_segs, n_lights, n_tris, n_sph, n_box, scene_kind, n_objs, small_tri;
     int det_bounded;   // every triangle has |e1| |e2| < 2^120 (ray_tri_nb's Newton reciprocal, xrt_api.cpp)
     DMedium medium;

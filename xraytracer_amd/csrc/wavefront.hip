@@ -1497,7 +1497,7 @@ struct HitRec {
 // (Src/scene.cpp:190-200, primitive.h:106-124).  Any-hit for shadow rays skips spheres of
 // area-light objects (Scene::occluded, Src/scene.cpp:202-211).
 template <bool ANY>
-__device__ __forceinline__ bool sphere_bvh(const LScene& L, v3 o, v3 d, float tmax, float& bt, int& bk, int& bj) {
+__device__ __forceinline__ bool sphere_bvh(const LScene& L, v3 o, v3 d, float tmax, float& bt, int& bk) {
     const v3 inv = rcp3(d);
     int i = 0;
     while (i < L.n_snode) {
@@ -1519,7 +1519,7 @@ __device__ __forceinline__ bool sphere_bvh(const LScene& L, v3 o, v3 d, float tm
                     if (t < tmax) return true;
                 } else {
                     const int k = kw & 0x3fffffff;
-                    if (t < bt || (t == bt && k < bk)) bt = t, bk = k, bj = j;
+                    if (t < bt || (t == bt && k < bk)) bt = t, bk = k;
                 }
             }
         }
@@ -1550,9 +1550,9 @@ __device__ __forceinline__ void closest_l(const KParams& P, const LScene& L, v3 
     } else if (SCN == SCN_SPHERE) {
         if (L.n_snode > 0) {
             float bt = kINF;
-            int bk = -1, bj = -1;
-            (void)sphere_bvh<false>(L, o, d, kINF, bt, bk, bj);
-            if (bk >= 0) h.t = bt, h.code = (1 << 28) | bk, h.surf = bj;   // surf: the winner's leaf-order index
+            int bk = -1;
+            (void)sphere_bvh<false>(L, o, d, kINF, bt, bk);
+            if (bk >= 0) h.t = bt, h.code = (1 << 28) | bk;
             return;
         }
         for (int k = 0; k < P.n_sph; ++k) {
@@ -1610,8 +1610,8 @@ __device__ __forceinline__ bool occluded_l(const KParams& P, const LScene& L, v3
     } else {
         if (SCN == SCN_SPHERE && L.n_snode > 0) {
             float bt = kINF;
-            int bk = -1, bj = -1;
-            return sphere_bvh<true>(L, o, d, tmax, bt, bk, bj);
+            int bk = -1;
+            return sphere_bvh<true>(L, o, d, tmax, bt, bk);
         }
         for (int sg = 0; sg < P.n_segs; ++sg) {
             const DSeg seg = P.segs[sg];
@@ -1643,12 +1643,6 @@ template <int SCN>
 __device__ __forceinline__ int surface_l(const LScene& L, v3 o, v3 d, const HitRec& h, Surf& S) {
     S.pos = S.ng = S.ns = S.dpdu = S.dpdv = mk(0, 0, 0);
     if (h.code < 0) return -1;
-    if (SCN == SCN_SPHERE && L.n_snode > 0) {   // sphere BVH in LDS: the leaf-order records (closest_l)
-        S.pos = ray_at(o, d, h.t);
-        S.ng = normalize(ray_at(o, d, h.t) - xyz(L.ssph[h.surf]));
-        S.ns = S.ng;
-        return L.sbo[h.surf];
-    }
     int surf = h.code, dp = (SCN == SCN_TRI) ? h.code : -1;
     float st = h.t, su = h.u, sv = h.v, du = h.u, dv = h.v;
     if (SCN == SCN_MIXED) surf = h.surf, dp = h.dp, st = h.st, su = h.su, sv = h.sv, du = h.du, dv = h.dv;
@@ -1769,20 +1763,15 @@ __global__ __launch_bounds__(BS, XRT_KSTEP_WAVES) void k_step(KParams P, const u
     lds_copy(const_cast<f4*>(L.bx), P.box, 2 * P.n_box, tid, BS);
     lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid, BS);
     if (SCN == SCN_SPHERE && P.n_snode > 0) {
-        // sphere BVH, leaf-order spheres and the shading records in LDS (step_layout); a hit's
-        // object is its record in the LDS table (L.obj), found by its leaf-order index
+        // sphere BVH in LDS; per-hit tables read from global memory (step_layout)
         L.snode = reinterpret_cast<const f4*>(lb + Lo.snode);
         L.ssph = reinterpret_cast<const f4*>(lb + Lo.ssph);
         L.sbk = reinterpret_cast<const int*>(lb + Lo.sbk);
-        L.sbo = reinterpret_cast<const int*>(lb + Lo.sbo);
         L.n_snode = P.n_snode;
         lds_copy(const_cast<f4*>(L.snode), P.snode, 2 * P.n_snode, tid, BS);
         lds_copy(const_cast<f4*>(L.ssph), P.ssph, P.n_sph, tid, BS);
         lds_copy(const_cast<int*>(L.sbk), P.sbk, P.n_sph, tid, BS);
-        lds_copy(const_cast<int*>(L.sbo), P.sbo, P.n_sph, tid, BS);
-        L.obj = reinterpret_cast<const DObj*>(lb + Lo.uobj);
-        lds_copy(const_cast<DObj*>(L.obj), P.uobj, P.n_uobj, tid, BS);
-        L.sph = P.sph, L.sobj = P.sph_obj;
+        L.sph = P.sph, L.sobj = P.sph_obj, L.obj = P.objs;
     } else {
         lds_copy(const_cast<f4*>(L.sph), P.sph, P.n_sph, tid, BS);
         lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid, BS);

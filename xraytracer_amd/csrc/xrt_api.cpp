@@ -43,7 +43,7 @@ struct xrt_ctx {
     // scene
     std::vector<DevBuf*> scene_bufs;
     DevBuf tri, tri_ng, tri_nrm, sph, sph_obj, box, objs, lights, segs, density, obj_box, obj_plane, bvh_node,
-        bvh_tri, snode, ssph, sbk, sbo, uobj, stri, sbox, splane, bvh4;
+        bvh_tri, snode, ssph, sbk, stri, sbox, splane, bvh4;
     KParams base{};
     StepObjs step_objs{};   // kernel-argument object records of the merged-trace schedule
     StepObjs sstep{};       // two-level trace: the small objects' records (KParams::sstep)
@@ -239,7 +239,7 @@ void xrt_destroy(xrt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->tri, &c->tri_ng, &c->tri_nrm, &c->sph, &c->sph_obj, &c->box, &c->objs, &c->lights,
-                     &c->segs, &c->density, &c->obj_box, &c->obj_plane, &c->bvh_node, &c->bvh_tri, &c->snode, &c->ssph, &c->sbk, &c->sbo, &c->uobj, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
+                     &c->segs, &c->density, &c->obj_box, &c->obj_plane, &c->bvh_node, &c->bvh_tri, &c->snode, &c->ssph, &c->sbk, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
                      &c->hit2, &c->hit3, &c->sh_o, &c->sh_d, &c->sh_c, &c->med, &c->med2, &c->nee, &c->state,
                      &c->sample_k, &c->depth, &c->occ, &c->rng_c, &c->rng_g, &c->ring, &c->c_seg, &c->c_shadow,
                      &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch, &c->kparams};
@@ -551,7 +551,6 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
     // far above the float error of Sphere::intersect's hit point (and of its
     // near-tangent discriminant), so a box test never drops a hit the linear scan accepts.
     P.snode = nullptr, P.ssph = nullptr, P.sbk = nullptr, P.n_snode = 0;
-    P.sbo = nullptr, P.uobj = nullptr, P.n_uobj = 0;
     if (P.scene_kind == SCN_SPHERE && P.n_sph >= kSphBvhMin && !exp_env("XRT_NO_BVH")) {
         const size_t ns = (size_t)P.n_sph;
         std::vector<float> mn(3 * ns), mx(3 * ns);
@@ -568,30 +567,17 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
         const BvhBuild B = build_bvh(mn.data(), mx.data(), (uint32_t)ns, kBvhLeaf, 1e-4f * diag + 1e-4f, kBvhMaxDepth);
         const std::vector<SkipNode> T = thread_bvh(B);
         std::vector<f4> bs(ns);
-        std::vector<int> bk(ns), bo(ns);
-        // the spheres' objects as distinct DObj records (the fused k_step reads a hit's material
-        // and light from LDS: C3's 1,001 sphere objects share two records)
-        std::vector<DObj> uo;
-        auto record = [&](const DObj& d) {
-            for (size_t u = 0; u < uo.size(); ++u)
-                if (std::memcmp(&uo[u], &d, sizeof(DObj)) == 0) return (int)u;
-            uo.push_back(d);
-            return (int)uo.size() - 1;
-        };
+        std::vector<int> bk(ns);
         for (size_t i = 0; i < ns; ++i) {
             const uint32_t k = B.order[i];
             bs[i] = sph[k];
             bk[i] = (int)k | (sph_obj[k] & (1 << 30));
-            bo[i] = record(objs[sph_obj[k] & 0x3fffffff]);
         }
         if ((rc = upload(c, c->snode, T.data(), T.size() * sizeof(SkipNode))) ||
             (rc = upload(c, c->ssph, bs.data(), bs.size() * sizeof(f4))) ||
-            (rc = upload(c, c->sbk, bk.data(), bk.size() * sizeof(int))) ||
-            (rc = upload(c, c->sbo, bo.data(), bo.size() * sizeof(int))) ||
-            (rc = upload(c, c->uobj, uo.data(), uo.size() * sizeof(DObj))))
+            (rc = upload(c, c->sbk, bk.data(), bk.size() * sizeof(int))))
             return rc;
         P.snode = as<f4>(c->snode), P.ssph = as<f4>(c->ssph), P.sbk = as<int>(c->sbk);
-        P.sbo = as<int>(c->sbo), P.uobj = as<DObj>(c->uobj), P.n_uobj = (int)uo.size();
         P.n_snode = (int)T.size();
     }
     c->obj_tri_first = std::move(tri_first);
