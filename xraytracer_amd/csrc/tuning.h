@@ -31,7 +31,7 @@
 
 // ---- the fused two-level schedule (k_step_merged<..., BVH = true>: C4)
 #ifndef XRT_BVH_WAVES
-#define XRT_BVH_WAVES 3      // 3 waves per SIMD (<= 168 VGPRs, no spills); 2: C4 -40%, 4: spills
+#define XRT_BVH_WAVES 4      // 4 waves per SIMD (128 VGPRs, ~30 spilled): C4 -11% vs 3 (no spills), 2: +40%
 #endif
 #ifndef XRT_BVH_LIVE64
 #define XRT_BVH_LIVE64 750000   // live slots above which two-level scenes take 64 slots per wave
@@ -46,7 +46,7 @@
 #define XRT_BVH_TOP 64       // top 4-wide BVH nodes kept in LDS (at most; kStepLds bounds it); 192: neutral
 #endif
 #ifndef XRT_DEEP_LEAF_BATCH
-#define XRT_DEEP_LEAF_BATCH 2  // leaf triangles whose loads are issued together (registers vs latency)
+#define XRT_DEEP_LEAF_BATCH 1  // leaf triangles whose loads are issued together (registers vs latency; 2: more spills)
 #endif
 #ifndef XRT_DEEP_SPREAD
 #define XRT_DEEP_SPREAD 1    // a node's overlapped leaf triangles dealt over the quad's lanes (C4 -12%)
