@@ -997,41 +997,37 @@ __device__ __forceinline__ int delta_step(const KParams& P, v3 o, v3 d, v3 thr, 
     const uint32_t channel = sample_wavelength(thr * tt, (vmaj - sa) * invMajorant, rng, pmf);
     const float s = -glibc_logf(smax(1.0f - rng.next(), 0.0f)) * invMajorant;
     t += s;
+    // the three outcomes share the transmittance and the throughput update: one expf and
+    // one quotient per collision however the wave's lanes split (same operands per lane)
+    int r = 0;
+    float x, fe = 1.0f;   // the expf argument's distance; the majorant factor of the pdf
+    v3 num = mk(0, 0, 0), Px = mk(1, 1, 1);
     if (t > t1 - kRAY_EPS) {
         pos = ray_at(o, d, t1 + kRAY_EPS);
         dir = d;
-        const float dist = s - (t - (t1 - kRAY_EPS));
-        const float e = glibc_expf(-majorant * dist);   // vexp((-vmaj) * dist)
-        const v3 tr = mk(e, e, e);
-        const v3 pdf = pmf * tr;
-        tt = tt * div3s(tr, pdf.x + pdf.y + pdf.z);
-        tm = isnan3(tt) ? mk(0, 0, 0) : tt;
-        return 0;
+        x = s - (t - (t1 - kRAY_EPS));
+    } else {
+        const float density = medium_density(M, ray_at(o, d, t));
+        const v3 sigma_s = scatter * density;
+        sa = absorb * density;
+        const v3 sigma_n = (vmaj - sa) - sigma_s;
+        const v3 den = sigma_s + sigma_n;
+        x = s, fe = majorant;
+        // P_s = sigma_s / (sigma_s + sigma_n): the acceptance test reads one component
+        r = rng.next() < comp(sigma_s, channel) / comp(den, channel) ? 1 : 3;
+        if (r == 1) {
+            pos = ray_at(o, d, t);
+            hg_sample(M.g, d, rng, dir);
+        }
+        num = r == 1 ? sigma_s : sigma_n;
+        Px = div3v(num, den);
     }
-    const float density = medium_density(M, ray_at(o, d, t));
-    const v3 sigma_s = scatter * density;
-    sa = absorb * density;
-    const v3 sigma_n = (vmaj - sa) - sigma_s;
-    const v3 den = sigma_s + sigma_n;
-    // P_s = sigma_s / (sigma_s + sigma_n): the acceptance test reads one component, the
-    // scattering branch all three (the same quotients, computed where they are used)
-    if (rng.next() < comp(sigma_s, channel) / comp(den, channel)) {
-        const v3 P_s = div3v(sigma_s, den);
-        pos = ray_at(o, d, t);
-        hg_sample(M.g, d, rng, dir);
-        const float e = glibc_expf(-majorant * s);   // vexp((-vmaj) * s): three equal arguments
-        const v3 tr = mk(e, e, e);
-        const v3 pdf = (pmf * (tr * majorant)) * P_s;
-        tt = tt * div3s(tr * sigma_s, pdf.x + pdf.y + pdf.z);
-        tm = isnan3(tt) ? mk(0, 0, 0) : tt;
-        return 1;
-    }
-    const v3 P_n = div3v(sigma_n, den);
-    const float e = glibc_expf(-majorant * s);
+    const float e = glibc_expf(-majorant * x);   // vexp((-vmaj) * x): three equal arguments
     const v3 tr = mk(e, e, e);
-    const v3 pdf = (pmf * (tr * majorant)) * P_n;
-    tt = tt * div3s(tr * sigma_n, pdf.x + pdf.y + pdf.z);
-    return 3;
+    const v3 pdf = r == 0 ? pmf * tr : (pmf * (tr * fe)) * Px;
+    tt = tt * div3s(r == 0 ? tr : tr * num, pdf.x + pdf.y + pdf.z);
+    if (r != 3) tm = isnan3(tt) ? mk(0, 0, 0) : tt;
+    return r;
 }
 // the whole walk (0, 1 or 2 as delta_step)
 __device__ int delta_track(const KParams& P, v3 o, v3 d, v3 thr, float& t, float t1, v3& tt, v3& sa, Rng& rng,
