@@ -47,10 +47,10 @@ constexpr uint32_t kVptEventDraws = XRT_VPT_EV_DRAWS;     // ... draws of an eve
                                            // collision draws <= 5; a lane with fewer words left stops early)
 constexpr uint32_t kVptEventPrefetch = XRT_VPT_EV_PF;     // ... reload the 8-word RNG window below this many
 constexpr bool kStepBlock512 = XRT_KSTEP_512 != 0;   // k_step of sphere-BVH scenes in 512-thread blocks
-constexpr uint32_t kStepRefill = 1;  // fused schedule: k_refill after every k_step
 constexpr uint32_t kVisitDraws = 13; // max RNG draws of one GI/Direct segment (4 lights)
-// fused schedule: a slot queues a refill when fewer than refill * visits * 13 + kRngVisit
-// words are left, so a GI/Direct slot never waits for words (KParams::rng_keep)
+// fused schedule: a slot's ring is twisted at the end of a step launch when fewer than
+// visits * 13 + kRngVisit words are left, so a GI/Direct slot never waits for words
+// (KParams::rng_keep)
 
 // slot state bits
 enum : uint32_t {

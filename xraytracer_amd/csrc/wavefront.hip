@@ -1739,6 +1739,7 @@ __global__ __launch_bounds__(BS, XRT_KSTEP_WAVES) void k_step(KParams P, const u
                                                   uint32_t* out_count, uint32_t* zero_count, uint32_t* req_count,
                                                   uint32_t visits) {
     extern __shared__ __attribute__((aligned(16))) f4 lds_step[];
+    __shared__ __attribute__((aligned(16))) uint32_t rbuf[BS / 64][kMT];   // wave_refill staging
     char* lb = reinterpret_cast<char*>(lds_step);
     const StepLayout Lo = step_layout(P);
     LScene L;
@@ -1782,8 +1783,9 @@ __global__ __launch_bounds__(BS, XRT_KSTEP_WAVES) void k_step(KParams P, const u
         const uint32_t s = i < it.n ? list[it.p * P.part_cap + i] : 0;
         uint32_t st = i < it.n ? P.state[s] : ST_DONE;
         bool want_req = false;
+        uint32_t g = 0;
         if (!(st & ST_DONE)) {
-        const uint32_t g = P.rng_g[s];
+        g = P.rng_g[s];
         Rng rng{P.ring + (size_t)s * kRing, P.rng_c[s]};
         uint32_t depth = P.depth[s];
         uint32_t k = P.sample_k[s];
@@ -2017,9 +2019,8 @@ __global__ __launch_bounds__(BS, XRT_KSTEP_WAVES) void k_step(KParams P, const u
             P.med2[s] = make_float4(tt.x, tt.y, tt.z, sa.z);
         }
         px[0] = acc.x, px[1] = acc.y, px[2] = acc.z;
-        // queue an RNG refill for k_refill (words ahead < rng_keep, once per request)
+        // RNG refill (words ahead < rng_keep <= 624): twisted by this wave below
         want_req = !(st & (ST_DONE | ST_RNGREQ)) && g - rng.c < P.rng_keep;
-        if (want_req) st |= ST_RNGREQ;
         P.state[s] = st;
         if (!(st & (ST_DONE | ST_REGEN))) {
             P.depth[s] = depth;
@@ -2035,10 +2036,12 @@ __global__ __launch_bounds__(BS, XRT_KSTEP_WAVES) void k_step(KParams P, const u
         if (nrej) P.c_rej[s] += nrej;
         if (nstall) P.c_stall[s] += nstall;
         }
-        // live list of the next round and refill requests (partitioned, one atomic per wave)
+        // live list of the next round (partitioned, one atomic per wave), then the wave's
+        // refills in-line (as k_step_merged: no k_refill launch between step launches)
         wave_append(!(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
-        wave_append(want_req, s, P.req + it.p * P.part_cap, req_count + it.p, lane);
+        wave_refill(P, want_req, s, g, lane, rbuf[tid >> 6]);
     }
+    (void)req_count;
 }
 
 // ======================================================= cooperative triangle trace ====
@@ -2329,8 +2332,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
         bool want_req = false;
         if (live) {
             px[0] = acc.x, px[1] = acc.y, px[2] = acc.z;
-            want_req = !(st & (ST_DONE | ST_RNGREQ)) && g - rng.c < P.rng_keep;
-            if (want_req) st |= ST_RNGREQ;
+            want_req = !(st & (ST_DONE | ST_RNGREQ)) && g - rng.c < P.rng_keep;   // twisted below
             P.state[s] = st;
             if (!(st & (ST_DONE | ST_REGEN))) {
                 P.depth[s] = depth;
@@ -2346,8 +2348,11 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_tri(const KPara
             if (nrej) P.c_rej[s] += nrej;
         }
         wave_append(live && !(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
-        wave_append(want_req, s, P.req + it.p * P.part_cap, req_count + it.p, lane);
+        // the wave's refills in-line through its trace scratch (idle now)
+        static_assert(sizeof(CoopWave) >= kMT * sizeof(uint32_t), "refill staging");
+        wave_refill(P, want_req, s, g, lane, reinterpret_cast<uint32_t*>(&W));
     }
+    (void)req_count;
 }
 
 // ================================================================== k_finish ====

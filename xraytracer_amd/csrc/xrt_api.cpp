@@ -905,8 +905,8 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     int poll_slot = 0;
     bool done = false;
     // k_step rotates three live counters: round i reads counts[i%3], appends to
-    // counts[(i+1)%3] and clears counts[(i+2)%3] for round i+1 (k_refill every kStepRefill
-    // rounds unless the kernel refills in-line).
+    // counts[(i+1)%3] and clears counts[(i+2)%3] for round i+1 (every step kernel twists its
+    // slots' rings in-line at the end of the launch: no k_refill after the seeding one).
     // segments per slot per step launch: kMergedVisits / kStepVisits unless the caller
     // sets visits_per_launch (results do not depend on it)
     const uint32_t merged_visits =
@@ -917,15 +917,13 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
                                  : merged               ? merged_visits
                                  : (volumetric && kVptEvents) ? kVptEventVisits
                                                         : kStepVisits;
-    // the merged kernel relies on one refill launch after every step launch (it clears
-    // ST_RNGREQ itself)
-    const uint32_t step_refill = merged ? 1u : kStepRefill;
     merged_refill = merged;
-    // a slot queues a refill when fewer words are left than the next `refill` launches can
-    // draw: the merged kernel draws at most step_merged_draws per segment and checks it
-    P.rng_keep = merged                      ? step_refill * step_visits * step_merged_draws(P) + step_merged_draws(P)
-                 : (volumetric && kVptEvents) ? step_refill * step_visits * kVptEventDraws + kRngVisit
-                                              : step_refill * step_visits * kVisitDraws + kRngVisit;
+    // a slot's ring is twisted at the end of a launch when fewer words are left than the next
+    // launch can draw: the merged kernel draws at most step_merged_draws per segment and
+    // checks it; k_step / k_step_tri check kRngVisit per visit
+    P.rng_keep = merged                      ? step_visits * step_merged_draws(P) + step_merged_draws(P)
+                 : (volumetric && kVptEvents) ? step_visits * kVptEventDraws + kRngVisit
+                                              : step_visits * kVisitDraws + kRngVisit;
     if (P.rng_keep > kMT) return set_err(c, XRT_ERR_INVALID, "visits_per_launch too large for the RNG ring");
     // device copy of the (now final) parameters for kernels that read them from memory
     if ((rc = ensure(c, c->kparams, sizeof(KParams)))) return rc;
@@ -966,11 +964,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
                                    req_counts + (epoch & 1) * kMaxParts, step_visits, blocks, c->stream);
             });
             if (e != hipSuccess) return hip_err(c, e, "k_step");
-            // the merged kernel refills its slots' rings itself (wave_refill)
-            if (!merged && it % step_refill == step_refill - 1) {
-                e = refill();
-                if (e != hipSuccess) return hip_err(c, e, "k_refill");
-            }
+            // both step kernels refill their slots' rings themselves (wave_refill)
         } else {
             live = counts_at(nxt);
             hipError_t e = launch(XRT_K_SHADE, [&] {
