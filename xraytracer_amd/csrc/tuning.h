@@ -22,6 +22,9 @@
 #ifndef XRT_STEP_WAVES
 #define XRT_STEP_WAVES 4     // min waves per SIMD of k_step_merged / k_step (<= 128 VGPRs; 3 or 5: C2 -5% / -9%)
 #endif
+#ifndef XRT_KSTEP_LDS_REFILL
+#define XRT_KSTEP_LDS_REFILL 2   // k_step in-line refill staged through LDS: 1 always, 2 except sphere-BVH scenes, 0 never
+#endif
 #ifndef XRT_KSTEP_512
 #define XRT_KSTEP_512 0      // C3: k_step in 512-thread blocks (one LDS copy per 8 waves): -2% 1 GPU, -9% 8 shards
 #endif

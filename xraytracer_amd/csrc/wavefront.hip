@@ -1739,7 +1739,6 @@ __global__ __launch_bounds__(BS, XRT_KSTEP_WAVES) void k_step(KParams P, const u
                                                   uint32_t* out_count, uint32_t* zero_count, uint32_t* req_count,
                                                   uint32_t visits) {
     extern __shared__ __attribute__((aligned(16))) f4 lds_step[];
-    __shared__ __attribute__((aligned(16))) uint32_t rbuf[BS / 64][kMT];   // wave_refill staging
     char* lb = reinterpret_cast<char*>(lds_step);
     const StepLayout Lo = step_layout(P);
     LScene L;
@@ -2039,7 +2038,16 @@ __global__ __launch_bounds__(BS, XRT_KSTEP_WAVES) void k_step(KParams P, const u
         // live list of the next round (partitioned, one atomic per wave), then the wave's
         // refills in-line (as k_step_merged: no k_refill launch between step launches)
         wave_append(!(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
-        wave_refill(P, want_req, s, g, lane, rbuf[tid >> 6]);
+        if constexpr (XRT_KSTEP_LDS_REFILL == 1 || (XRT_KSTEP_LDS_REFILL == 2 && SCN != SCN_SPHERE)) {
+            __shared__ __attribute__((aligned(16))) uint32_t rbuf[BS / 64][kMT];   // wave_refill staging
+            wave_refill(P, want_req, s, g, lane, rbuf[tid >> 6]);
+        } else {
+            // sphere-BVH scenes: twisted from global memory (L2), no LDS buffer beside the
+            // scene's ~45 KB (3 blocks per CU instead of 2)
+            uint32_t gn = g;
+            wave_refill(want_req, s, gn, P.ring, lane);
+            if (want_req) P.rng_g[s] = gn;
+        }
     }
     (void)req_count;
 }
