@@ -139,6 +139,8 @@ def hip_kernel_name(kid, sched, scene):
     rocprofv3 reports, which the PMC summaries are keyed by)."""
     from xraytracer_amd import abi
     if kid == abi.XRT_K_STEP:
+        if sched == abi.XRT_SCHED_PIXEL:
+            return "k_pixel"
         if sched in (abi.XRT_SCHED_STEP_MERGED, abi.XRT_SCHED_STEP_BVH):   # k_step_merged<..., BVH>
             return "k_step_merged"
         return "k_step_tri" if sched == abi.XRT_SCHED_STEP_TRI else "k_step"
@@ -166,7 +168,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=None, help="override the CPU sample's spp")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
-    ap.add_argument("--schedule", default="auto", choices=("auto", "wavefront"))
+    ap.add_argument("--schedule", default="auto", choices=("auto", "step", "wavefront"))
     ap.add_argument("--traffic", default=None, help="default profiles/traffic_<CONFIG>.json")
     ap.add_argument("--pmc", default=None, help="default profiles/pmc_<CONFIG>.json")
     args = ap.parse_args()

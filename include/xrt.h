@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 10
+#define XRT_ABI_VERSION 11
 
 /* ---- status codes ---------------------------------------------------------------- */
 enum {
@@ -135,6 +135,8 @@ enum {
     XRT_FLAG_DEEP_SINGLE = 32u, /* two-level traces: walk the BVH with one lane per queued ray  */
     XRT_FLAG_DEEP_QUAD = 64u,   /* ... with four lanes per ray (the default); results never
                                    depend on either                                            */
+    XRT_FLAG_NO_PIXEL = 128u,   /* Direct / Normal: the per-slot fused schedule (k_step) instead
+                                   of pixel-parallel sample chains (k_pixel); same results     */
     XRT_FLAG_ACCUMULATE = 16u  /* Renderer::render's in-place contract (Src/renderer.cpp:75,98):
                                   each owned pixel starts from the value already in the output
                                   buffer (Image::addPixel adds to it in sample order), then
@@ -165,11 +167,14 @@ enum {
 
 /* device schedules: multi-pass wavefront (k_shade + k_trace), fused per-slot k_step with
  * the scene in LDS, its triangle-scene form with cooperative (ray, triangle) traces, that
- * form with one merged trace (shadow rays + next extension ray) per segment, and the merged
- * form for two-level scenes (small objects in LDS, a big mesh's BVH walked by the wave) */
+ * form with one merged trace (shadow rays + next extension ray) per segment, the merged
+ * form for two-level scenes (small objects in LDS, a big mesh's BVH walked by the wave), and
+ * for the one-trace integrators (Direct, Normal) pixel-parallel sample chains: one wave per
+ * pixel evaluates 64 candidate samples at once and keeps those on the pixel's chain (k_pixel;
+ * timed as XRT_K_STEP) */
 enum {
     XRT_SCHED_WAVEFRONT = 0, XRT_SCHED_STEP = 1, XRT_SCHED_STEP_TRI = 2, XRT_SCHED_STEP_MERGED = 3,
-    XRT_SCHED_STEP_BVH = 4
+    XRT_SCHED_STEP_BVH = 4, XRT_SCHED_PIXEL = 5
 };
 
 typedef struct {

@@ -51,7 +51,7 @@ def renderer():
     r.close()
 
 
-def render_like_bench(r, cfg, spp):
+def render_like_bench(r, cfg, spp, schedule="auto"):
     """bench.py's step: xrt_render_device into a torch tensor on cuda:0, schedule auto,
     HIP-event timing on, shard 0 of 1."""
     import torch
@@ -63,7 +63,7 @@ def render_like_bench(r, cfg, spp):
     r.upload(scene)
     fb = torch.full((h, w, 3), 7.0, dtype=torch.float32, device="cuda:0")   # overwritten, not added to
     r.render_device(scene, w, h, fb.data_ptr(), after_stream=torch.cuda.current_stream().cuda_stream,
-                    timing=True, schedule="auto")
+                    timing=True, schedule=schedule)
     img = fb.cpu().numpy()
     ref, st = pyoracle.render(scene, w, h, spp)
     return img, ref, st, r.stats
@@ -101,11 +101,12 @@ def test_c2_headline_across_launches(renderer):
 
 
 def test_c3_geometry_across_launches(renderer):
-    """VERDICT r2 #1 for C3 (1,000 spheres, 1280x720, Direct): at 96 spp every slot needs 96
-    visits, three rounds of k_step (32 visits per launch), each twisting its slots' RNG rings
-    at its end (in-line refills: no k_refill launch after the seeding one).  The oracle's linear
-    sphere scan is slow, so a row subset (rows y % 64 == 21) of the full-frame GPU image is
-    compared bit for bit."""
+    """VERDICT r2 #1 for C3 (1,000 spheres, 1280x720, Direct) under the per-slot schedule
+    (XRT_FLAG_NO_PIXEL; the default is k_pixel, tests/test_gpu_pixel.py): at 96 spp every
+    slot needs 96 visits, three rounds of k_step (32 visits per launch), each twisting its
+    slots' RNG rings at its end (in-line refills: no k_refill launch after the seeding one).
+    The oracle's linear sphere scan is slow, so a row subset (rows y % 64 == 21) of the
+    full-frame GPU image is compared bit for bit."""
     import torch
 
     c = scenes.CONFIGS["C3"]
@@ -115,7 +116,7 @@ def test_c3_geometry_across_launches(renderer):
     renderer.upload(scene)
     fb = torch.full((h, w, 3), 7.0, dtype=torch.float32, device="cuda:0")
     renderer.render_device(scene, w, h, fb.data_ptr(), after_stream=torch.cuda.current_stream().cuda_stream,
-                           timing=True, schedule="auto")
+                           timing=True, schedule="step")
     g = renderer.stats
     img = fb.cpu().numpy()
     assert g.schedule == abi.XRT_SCHED_STEP and g.partitions == partitions(w * h)
@@ -128,9 +129,9 @@ def test_c3_geometry_across_launches(renderer):
 
 
 def test_c3_row_shard(renderer):
-    """C3 as one rank of 8 renders it (rows y % 8 == 3: 90 x 1280 slots, 224 partitions — a
-    grid that is not a power-of-two multiple of the partitions), 8 spp, zeros elsewhere, rows
-    y % 64 == 3 bit-exact against the oracle."""
+    """C3 as one rank of 8 renders it under the per-slot schedule (rows y % 8 == 3: 90 x 1280
+    slots, 224 partitions — a grid that is not a power-of-two multiple of the partitions),
+    8 spp, zeros elsewhere, rows y % 64 == 3 bit-exact against the oracle."""
     import torch
 
     c = scenes.CONFIGS["C3"]
@@ -140,7 +141,7 @@ def test_c3_row_shard(renderer):
     renderer.upload(scene)
     fb = torch.full((h, w, 3), 7.0, dtype=torch.float32, device="cuda:0")
     renderer.render_device(scene, w, h, fb.data_ptr(), after_stream=torch.cuda.current_stream().cuda_stream,
-                           timing=True, schedule="auto", shard_index=3, shard_count=8)
+                           timing=True, schedule="step", shard_index=3, shard_count=8)
     g = renderer.stats
     img = fb.cpu().numpy()
     assert g.schedule == abi.XRT_SCHED_STEP and g.partitions == partitions(90 * 1280) == 224
@@ -152,11 +153,13 @@ def test_c3_row_shard(renderer):
     compare(img[3::64], ref[3::64])
 
 
-def test_c3_geometry(renderer):
-    """C3 (1,000 spheres + sphere light, 1280x720, Direct): fused k_step with the LDS
-    skip-link sphere BVH, 1024 partitions."""
-    img, ref, st, g = render_like_bench(renderer, "C3", 1)
-    assert g.schedule == abi.XRT_SCHED_STEP
+@pytest.mark.parametrize("schedule", ["auto", "step"])
+def test_c3_geometry(renderer, schedule):
+    """C3 (1,000 spheres + sphere light, 1280x720, Direct), full frame at 1 spp: the pixel
+    schedule (the bench's) and the per-slot fused k_step with the LDS skip-link sphere BVH
+    over 1024 partitions."""
+    img, ref, st, g = render_like_bench(renderer, "C3", 1, schedule=schedule)
+    assert g.schedule == (abi.XRT_SCHED_PIXEL if schedule == "auto" else abi.XRT_SCHED_STEP)
     assert g.partitions == partitions(1280 * 720)
     compare(img, ref)
     counters_equal(g, st)
@@ -242,6 +245,48 @@ def test_c4_row_shard(renderer):
     ref, _ = c4_reference()
     k, n = C4_SUB
     compare(img[k::n], ref[k::n])
+
+
+C4_TWIST_SPP = 96
+
+
+@functools.lru_cache(maxsize=1)
+def c4_twist_reference():
+    s = scenes.cornell_spheremesh(64, 36, n_theta=24, n_phi=24)
+    return s, pyoracle.render(s, 64, 36, C4_TWIST_SPP)
+
+
+@pytest.mark.parametrize("spw,shard", [(0, None), (64, None), (32, None), (16, None), (0, 3)])
+def test_c4_kernel_twists_in_launch(renderer, spw, shard):
+    """the benched C4 kernel k_step_merged<GI, ..., BVH> twisting its slots'
+    RNG rings at the end of a launch (wave_refill staged through the MergedWave LDS it shares
+    with the BVH top nodes and the quads' stacks).  A slot asks for a twist once fewer than
+    rng_keep = 64 * 8 + 8 = 520 words are left, i.e. after ~104 draws, ~15 samples of C4's
+    ~7 draws each, so at 96 spp nearly every slot twists in-launch at least once.  The C4 scene
+    family with a 24 x 24 sphere mesh (1,152 + 36 triangles: the mesh goes into the BVH), at
+    every slots-per-wave layout the library picks from (64, 32, 16; auto = 16 for 2,304
+    slots) and as row shard 3 of 8: bit-exact, counters equal (Src/sampler.h:16-50,
+    Src/renderer.cpp:29-81)."""
+    s, (ref, st) = c4_twist_reference()
+    assert s.desc.n_tris == 24 * 24 * 2 + 36
+    renderer.spp = C4_TWIST_SPP
+    renderer.upload(s)
+    kw = {} if shard is None else dict(shard_index=shard, shard_count=8)
+    img = renderer.render(s, 64, 36, timing=True, schedule="auto", slots_per_wave=spw, **kw)
+    g = renderer.stats
+    assert g.schedule == abi.XRT_SCHED_STEP_BVH
+    assert g.launches[abi.XRT_K_REFILL] == 1 and g.launches[abi.XRT_K_STEP] >= 2, list(g.launches)
+    assert g.rng_twists - g.path_slots > g.path_slots // 4, (g.rng_twists, g.path_slots)
+    if spw:
+        assert g.layout_launches[abi.LAYOUTS.index(spw)] == g.launches[abi.XRT_K_STEP]
+    if shard is None:
+        compare(img, ref)
+        counters_equal(g, st)
+    else:
+        owned = np.zeros(36, bool)
+        owned[shard::8] = True
+        assert np.all(img[~owned] == 0)
+        compare(img[owned], ref[owned])
 
 
 def test_c5_full_frame(renderer):

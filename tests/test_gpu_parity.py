@@ -38,8 +38,10 @@ def renderer():
 def sched(request):
     """Every device schedule: "auto" runs the fused LDS-resident kernels for scenes that fit
     (every scene below except the C4 sphere mesh) — small triangle scenes with merged
-    shadow + extension traces (k_step_merged); "step_tri" forces the per-ray-kind
-    cooperative traces (k_step_tri) for those; "wavefront" forces k_shade + k_trace."""
+    shadow + extension traces (k_step_merged), Direct / Normal as pixel-parallel sample
+    chains (k_pixel); "step_tri" forces the per-slot kernels with per-ray-kind cooperative
+    traces (k_step_tri) for triangle scenes and k_step for the others; "wavefront" forces
+    k_shade + k_trace."""
     return request.param
 
 
@@ -47,7 +49,7 @@ EXPECT_TRI = {"auto": abi.XRT_SCHED_STEP_MERGED, "step_tri": abi.XRT_SCHED_STEP_
               "wavefront": abi.XRT_SCHED_WAVEFRONT}
 
 
-GPU_ONLY = ("slots_per_wave", "visits_per_launch", "group", "deep")   # launch geometry, not semantics
+GPU_ONLY = ("slots_per_wave", "visits_per_launch", "group", "deep", "timing")   # launch geometry, not semantics
 
 
 def render_both(r, scene, w, h, spp, schedule="auto", **kw):
@@ -264,7 +266,7 @@ def test_merged_segments_per_launch(renderer, visits):
     counters (GI and Direct; one and two lights)."""
     s = scenes.cornell(24, 18)
     for kw in ({}, {"integrator": "direct"}, {"max_depth": 5}):
-        img, ref, st = render_both(renderer, s, 24, 18, 6, visits_per_launch=visits, **kw)
+        img, ref, st = render_both(renderer, s, 24, 18, 6, visits_per_launch=visits, schedule="step", **kw)
         compare(img, ref)
         g = renderer.stats
         assert g.schedule == abi.XRT_SCHED_STEP_MERGED and g.visits_per_launch == visits
@@ -278,7 +280,7 @@ def test_merged_slots_per_wave(renderer, spw, group):
     (cooperative passes) — render the same image and counters as full waves."""
     s = scenes.cornell(40, 30)
     for kw in ({}, {"integrator": "direct"}):
-        img, ref, st = render_both(renderer, s, 40, 30, 5, slots_per_wave=spw, group=group, **kw)
+        img, ref, st = render_both(renderer, s, 40, 30, 5, slots_per_wave=spw, group=group, schedule="step", **kw)
         compare(img, ref)
         g = renderer.stats
         assert g.schedule == abi.XRT_SCHED_STEP_MERGED
@@ -306,7 +308,8 @@ def test_c3_spheres_direct(renderer, sched):
     s = scenes.spheres(160, 90)
     img, ref, st = render_both(renderer, s, 160, 90, 4, schedule=sched)
     compare(img, ref)
-    assert renderer.stats.schedule == (abi.XRT_SCHED_WAVEFRONT if sched == "wavefront" else abi.XRT_SCHED_STEP)
+    assert renderer.stats.schedule == {"wavefront": abi.XRT_SCHED_WAVEFRONT, "step_tri": abi.XRT_SCHED_STEP,
+                                       "auto": abi.XRT_SCHED_PIXEL}[sched]
     assert renderer.stats.shadow_rays == st["shadow_rays"]
 
 
@@ -354,6 +357,30 @@ def test_normal_integrator_on_medium_box(renderer, sched):
     s = scenes.smoke(32, 24)
     img, ref, _ = render_both(renderer, s, 32, 24, 2, integrator="normal", schedule=sched)
     compare(img, ref)
+
+
+@pytest.mark.parametrize("integ,schedule", [("indirect", "auto"), ("normal", "step"), ("gi", "step_tri")])
+def test_kstep_refill_staging_beside_a_large_scene(renderer, integ, schedule):
+    """k_step stages its in-line RNG refill through LDS right after the scene carve
+    (kstep_refill_off).  A 520-triangle scene (Cornell + two 242-triangle sphere meshes, none
+    large enough for the BVH) fills ~59 KB of the 64 KiB scene budget, so scene + staging
+    exceed 64 KiB; the launch is sized for both.  Rings are twisted in-launch (64 spp)."""
+    s = scenes.SceneBundle()
+    s.load_obj(scenes.CORNELL_OBJ)
+    s.add_quad_light("QuadLight", (343.0, 548.0, 227.0), (343.0, 548.0, 332.0), (213.0, 548.0, 227.0),
+                     (25.0, 25.0, 25.0))
+    s.add_sphere_mesh("mesh_a", (150.0, 420.0, 400.0), 90.0, 11, 11, (0.58, 0.58, 0.58))
+    s.add_sphere_mesh("mesh_b", (400.0, 120.0, 300.0), 70.0, 11, 11, (0.3, 0.6, 0.5))
+    s.flatten()
+    s.camera = scenes.pinhole(scenes.CORNELL_C2W, 60.0, 40, 30)
+    assert s.desc.n_tris == 36 + 2 * 242
+    img, ref, st = render_both(renderer, s, 40, 30, 64, integrator=integ, max_depth=3, schedule=schedule,
+                               timing=True)
+    compare(img, ref)
+    g = renderer.stats
+    assert g.schedule == abi.XRT_SCHED_STEP   # the layout leaves no room for k_step_tri's scratch
+    assert (g.segments, g.shadow_rays, g.draws) == (st["segments"], st["shadow_rays"], st["draws"])
+    assert g.launches[abi.XRT_K_REFILL] == 1 and g.rng_twists - g.path_slots > g.path_slots // 4
 
 
 @pytest.mark.parametrize("deep", ["fused", "single", "quad"])

@@ -17,7 +17,7 @@ if os.environ.get("XRT_LIB"):   # experiment builds (csrc/Makefile `variant` -> 
     _v = os.path.join(HERE, "variants", os.environ["XRT_LIB"])
     LIB_PATH = _v if os.path.exists(_v) else os.path.join(HERE, os.environ["XRT_LIB"])
 
-XRT_ABI_VERSION = 10  # include/xrt.h XRT_ABI_VERSION
+XRT_ABI_VERSION = 11  # include/xrt.h XRT_ABI_VERSION
 XRT_OK = 0
 XRT_OBJ_MESH, XRT_OBJ_SPHERE, XRT_OBJ_BOX = 0, 1, 2
 XRT_LIGHT_QUAD, XRT_LIGHT_TRIANGLE, XRT_LIGHT_SPHERE = 0, 1, 2
@@ -26,9 +26,10 @@ XRT_INTEGRATOR_GI, XRT_INTEGRATOR_DIRECT, XRT_INTEGRATOR_VPT = 0, 1, 2
 XRT_INTEGRATOR_INDIRECT, XRT_INTEGRATOR_NORMAL, XRT_INTEGRATOR_VPT_NEE = 3, 4, 5
 XRT_MEDIUM_HETEROGENEOUS, XRT_MEDIUM_HOMOGENEOUS_MIS, XRT_MEDIUM_HOMOGENEOUS_ACHROMATIC, XRT_MEDIUM_HOMOGENEOUS_NOMIS = 0, 1, 2, 3
 XRT_FLAG_TIMING, XRT_FLAG_WAVEFRONT, XRT_FLAG_NO_MERGED, XRT_FLAG_NO_GROUP, XRT_FLAG_ACCUMULATE = 1, 2, 4, 8, 16
-XRT_FLAG_DEEP_SINGLE, XRT_FLAG_DEEP_QUAD = 32, 64
+XRT_FLAG_DEEP_SINGLE, XRT_FLAG_DEEP_QUAD, XRT_FLAG_NO_PIXEL = 32, 64, 128
 XRT_SCHED_WAVEFRONT, XRT_SCHED_STEP, XRT_SCHED_STEP_TRI, XRT_SCHED_STEP_MERGED, XRT_SCHED_STEP_BVH = 0, 1, 2, 3, 4
-SCHEDULE_NAMES = ("wavefront", "step", "step_tri", "step_merged", "step_bvh")
+XRT_SCHED_PIXEL = 5
+SCHEDULE_NAMES = ("wavefront", "step", "step_tri", "step_merged", "step_bvh", "pixel")
 XRT_K_SEED, XRT_K_TRACE, XRT_K_SHADE, XRT_K_FINISH, XRT_K_STEP, XRT_K_REFILL, XRT_K_DEEP, XRT_K_COUNT = \
     0, 1, 2, 3, 4, 5, 6, 7
 LAYOUTS = (64, 32, 16, 8, 4)   # xrt_stats.layout_launches: slots per wave

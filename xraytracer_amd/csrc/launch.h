@@ -33,6 +33,12 @@ hipError_t launch_shade(const KParams& P, const uint32_t* list, const uint32_t* 
 // fused schedule (k_step): LDS bytes it needs for this scene, 0 = scene too large for it
 size_t step_lds_bytes(const KParams& P);
 bool use_step_tri(const KParams& P);   // triangle scene: k_step_tri (cooperative traces)
+// pixel-parallel sample chains (pixel.hip): Direct / Normal scenes that fit the LDS scene
+// carve; one launch renders every pixel of the shard (after k_seed, before k_finish), taking
+// pixels from the counter at `work` (zeroed by the launcher)
+bool use_pixel(const KParams& P);
+size_t pix_lds_bytes(const KParams& P);
+hipError_t launch_pixel(const KParams& P, uint32_t* work, hipStream_t st);
 // up to `visits` path segments per live slot; appends survivors to out (partitioned
 // counters out_count), low-RNG slots to P.req (req_count); clears zero (next-next round)
 // dP: device copy of P (the triangle-scene kernel reads its parameters from memory)

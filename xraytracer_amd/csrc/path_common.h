@@ -451,6 +451,27 @@ __device__ __forceinline__ int surface(const KParams& P, uint32_t s, v3 o, v3 d,
     return __float_as_int(P.box[2 * idx].w);
 }
 
+// Component-wise quotients a / b and a / (b, b, b) with one division when the numerators (and
+// denominators) are the same bits — achromatic media and throughputs (C5) — else three; the
+// same IEEE quotients either way.  Bit equality, not ==: +0 and -0 differ in the quotient.
+__device__ __forceinline__ bool same3(v3 a) {
+    return __float_as_uint(a.x) == __float_as_uint(a.y) && __float_as_uint(a.y) == __float_as_uint(a.z);
+}
+__device__ __forceinline__ v3 div3s(v3 a, float b) {
+    if (same3(a)) {
+        const float q = a.x / b;
+        return mk(q, q, q);
+    }
+    return a / b;
+}
+__device__ __forceinline__ v3 div3v(v3 a, v3 b) {
+    if (same3(a) && same3(b)) {
+        const float q = a.x / b.x;
+        return mk(q, q, q);
+    }
+    return a / b;
+}
+
 // AreaLight::Le (Src/light.h:62-69)
 __device__ __forceinline__ v3 light_Le(const DLight& L, v3 ns, v3 wi) {
     return dot(wi, ns) < 0.0f ? mk(L.Le[0], L.Le[1], L.Le[2]) : mk(0, 0, 0);

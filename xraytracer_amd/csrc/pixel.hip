@@ -1,0 +1,290 @@
+// pixel.hip — pixel-parallel sample chains for the one-trace integrators
+// (DirectIntegrator, Src/integrator.h:82-119; NormalIntegrator, :22-74).
+//
+// NormalRenderer::doRender (Src/renderer.cpp:29-81) runs a pixel's samples in order on one
+// mt19937 stream, so every other schedule gives a pixel one lane and runs its samples one
+// after the other: a frame is as long as its slowest pixel's chain of traces, and a row
+// shard of an 8-GPU frame leaves most of the chip idle.  For these two integrators a
+// sample's draw count depends only on its camera ray:
+//   Direct : 2 jitter words, then 2 words per area light iff the camera ray hits a surface
+//            that is not an area light (every light's sample() draws exactly 2, whether or
+//            not it returns pdf 0: Src/light.cpp:21-68, light.h:157-197)
+//   Normal : 2 jitter words, nothing else
+// so the stream offset of sample k+1 is f(o_k) = o_k + 2 + 2·NL·hit(o_k), and hit(o) is a
+// function of the two words at o alone.  One wave takes one pixel and evaluates a window of
+// 64 candidate offsets o, o+2, ..., o+126 at once — every lane traces the camera ray its
+// candidate's jitter words give — then walks the chain o -> f(o) through the window with
+// scalar bit operations on the ballot of surface hits.  The candidates on the chain are the
+// pixel's next samples, in order: they shade (light samples from the words after their
+// jitter, shadow rays), pass the reference's NaN / Inf / negative check, and are added to the
+// pixel's running sum one after the other in sample order by three lanes (one per channel),
+// exactly Image::addPixel's sequence.  The candidates off the chain (offsets inside another
+// sample's light words) are discarded.  Every sample therefore draws the same words, traces
+// the same rays and adds the same floats as the reference: the image, the counters and the
+// final stream cursor are bit-identical (tests/test_gpu_pixel.py).
+//
+// The 64 camera rays of a window leave one pixel through nearly the same point, so the
+// wave's traversals are coherent (the per-slot k_step walks 64 unrelated pixels, and a
+// visit lasts as long as its slowest lane's walk), and the frame has one work item per
+// pixel instead of one serial chain per pixel: a row shard of 1/8 of the pixels still
+// fills the chip.  Cost: the off-chain candidates' camera traces (a fraction h/(1+h) of
+// the candidates for a surface-hit rate h and one light).
+//
+// The stream lives in LDS: each wave keeps its pixel's last 624 words in a circular buffer
+// (x[i] at st[i % 624]; the state k_seed wrote is x[0..623]) and generates 128 words at a
+// time before a window needs them — x[i] = x[i-227] ^ mix(x[i-624], x[i-623]) for the
+// 128 words i in [g, g+128), whose inputs are all generated and none of which are
+// overwritten before they are read (i - 227 >= g - 227 lies outside the chunk's slots).
+// Persistent waves take pixels from an atomic counter until none are left.
+#include <hip/hip_runtime.h>
+
+#include "lscene.h"
+#include "path_common.h"
+
+namespace xrt {
+
+constexpr int kPixBlock = XRT_PIX_BLOCK;           // threads per block: 8 waves share one LDS scene copy
+constexpr uint32_t kPixSumStride = 68;             // ordered-sum buffer row (floats): 64 + 4, rows on other banks
+constexpr uint32_t kPixWaveLds = (kMT + 3 * kPixSumStride) * 4;   // per wave: stream window + sum buffer
+
+// the words generated per chunk: one pair per lane
+constexpr uint32_t kPixChunk = 128;
+
+// LDS-fed UniformSampler of one lane: x[c], x[c+1], ... from the wave's circular buffer.  The
+// window logic guarantees every word it is asked for has been generated and not overwritten.
+struct LdsRng {
+    const uint32_t* st;
+    uint32_t i;   // c % kMT
+    __device__ __forceinline__ float next() {
+        const uint32_t y = st[i];
+        i = (i + 1 == kMT) ? 0u : i + 1;
+        return canonical(mt_temper(y));
+    }
+};
+
+// x[g .. g+127] into the circular buffer (x[g-624 .. g-1] in it): lane l makes x[g+2l] and
+// x[g+2l+1] (libstdc++ _M_gen_rand's recurrence, one word at a time).  Every operand is read
+// before any lane writes: lane l's second word needs x[g+2l+2-624], which lane l+1 replaces.
+__device__ __forceinline__ void pix_gen(uint32_t* st, uint32_t g, int lane) {
+    uint32_t i0 = g % kMT + 2u * (uint32_t)lane;
+    if (i0 >= kMT) i0 -= kMT;
+    const uint32_t i1 = i0 + 1u;   // g and kMT are even: a pair never wraps
+    uint32_t i2 = i1 + 1u;
+    if (i2 >= kMT) i2 -= kMT;
+    uint32_t j0 = i0 + (kMT - 227u);   // x[i - 227] sits at (i + 397) % 624 (odd: j0 + 1 may wrap)
+    if (j0 >= kMT) j0 -= kMT;
+    uint32_t j1 = j0 + 1u;
+    if (j1 >= kMT) j1 -= kMT;
+    const uint32_t a0 = st[i0], a1 = st[i1], a2 = st[i2], b0 = st[j0], b1 = st[j1];
+    wave_sync();
+    st[i0] = b0 ^ mt_mix(a0, a1);
+    st[i1] = b1 ^ mt_mix(a1, a2);
+    wave_sync();
+}
+
+// LDS bytes of the pixel schedule: the scene carve, then kPixWaveLds per wave
+__host__ __device__ inline uint32_t pix_wave_off(const KParams& P) { return (step_layout(P).total + 15u) & ~15u; }
+
+template <int SCN, int INTEG>
+__global__ __launch_bounds__(kPixBlock, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t* __restrict__ work) {
+    extern __shared__ __attribute__((aligned(16))) f4 lds_pix[];
+    char* lb = reinterpret_cast<char*>(lds_pix);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const LScene L = load_lscene(P, lb, tid, kPixBlock);
+    uint32_t* st = reinterpret_cast<uint32_t*>(lb + pix_wave_off(P) + (tid >> 6) * kPixWaveLds);
+    float* sum = reinterpret_cast<float*>(st + kMT);
+    __syncthreads();
+    // words a surface hit draws beyond its jitter, in pairs: one pair per area light (Direct)
+    const uint32_t NLD = INTEG == XRT_INTEGRATOR_DIRECT ? (uint32_t)P.n_lights : 0u;
+    for (;;) {
+        uint32_t s = 0;
+        if (lane == 0) s = atomicAdd(work, 1u);
+        s = (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
+        if (s >= P.n_slots) break;   // every wave reaches this: the grid drains
+        const uint32_t col = s % P.width, row = P.shard_index + P.shard_count * (s / P.width);
+        // the seeded state x[0..623] (k_seed) -> the circular buffer, 16 B per lane and load
+        {
+            const u32x4* src = reinterpret_cast<const u32x4*>(P.ring + (size_t)s * kRing);
+            u32x4 v[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                v[k] = __builtin_nontemporal_load(src + min((uint32_t)lane + 64u * k, kMT / 4 - 1u));
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                if ((uint32_t)lane + 64u * k < kMT / 4) reinterpret_cast<u32x4*>(st)[lane + 64 * k] = v[k];
+            wave_sync();
+        }
+        float* px = P.fb + 3 * ((size_t)col + (size_t)P.width * row);
+        float acc = lane < 3 ? px[lane] : 0.0f;   // lane c < 3: channel c of the running sum
+        uint32_t o = kMT, g = kMT, k = 0;        // next draw x[o]; x[0 .. g) generated
+        uint32_t nsh = 0, nrej = 0;
+        while (k < P.spp) {
+            const uint32_t rem = P.spp - k;
+            // candidates that can lie on the chain: rem samples advance at most 1 + NLD each
+            const uint32_t span = rem >= 64u ? 64u : min(64u, rem * (1u + NLD));
+            const uint32_t need = o + 2u * span + 2u * NLD;   // words this window may read
+            while (g < need) {
+                pix_gen(st, g, lane);
+                g += kPixChunk;
+            }
+            // the candidate sample at offset o + 2·lane: jitter, camera ray, Scene::intersect
+            // (Src/renderer.cpp:44-53)
+            const bool cand = (uint32_t)lane < span;
+            uint32_t ci = (o % kMT) + 2u * (uint32_t)lane;
+            if (ci >= kMT) ci -= kMT;
+            LdsRng rng{st, ci};
+            v3 ro = mk(0, 0, 0), rd = mk(0, 0, 0);
+            Surf S;
+            int obj = -1, kind = 0;   // 0 miss, 1 area light, 2 surface
+            if (cand) {
+                const float u = div_w(P, (float)(int)col + rng.next());
+                const float v = div_h(P, (float)(int)row + rng.next());
+                camera_ray(P, u, v, ro, rd);
+                HitRec h;
+                closest_l<SCN>(P, L, ro, rd, h);
+                obj = surface_l<SCN>(L, ro, rd, h, S);
+                kind = obj < 0 ? 0 : (L.obj[obj].light >= 0 ? 1 : 2);
+            }
+            // the chain through the window (scalar): from candidate 0 (the next sample), a
+            // sample at candidate q moves to q + 1, or to q + 1 + NLD after a surface hit
+            const uint64_t smask = NLD ? (uint64_t)__ballot(kind == 2) : 0ull;
+            uint64_t M = 0;
+            uint32_t cnt = 0, pos = 0;
+            while (pos < 64u && cnt < rem) {
+                const uint64_t ahead = smask >> pos;
+                const uint32_t q = ahead ? pos + (uint32_t)__builtin_ctzll(ahead) : 64u;
+                uint32_t run = q - pos;   // samples without a surface hit, then the one at q
+                if (run > rem - cnt) run = rem - cnt;
+                M |= (run == 64u ? ~0ull : ((1ull << run) - 1ull)) << pos;
+                cnt += run;
+                pos += run;
+                if (cnt == rem || q == 64u) break;   // sample budget reached, or the window ends
+                M |= 1ull << q;   // pos == q here
+                ++cnt;
+                pos = q + 1u + NLD;
+            }
+            const bool member = (M >> lane) & 1ull;
+            v3 rad = mk(0, 0, 0);
+            if (member) {
+                if (INTEG == XRT_INTEGRATOR_DIRECT) {
+                    // DirectIntegrator::integrate (Src/integrator.h:82-119)
+                    if (kind == 0) {
+                        rad = mk((float)0.18, (float)0.18, (float)0.18);
+                    } else if (kind == 1) {
+                        rad = light_Le(L.light[L.obj[obj].light], S.ns, rd);
+                    } else {
+                        const DObj& ob = L.obj[obj];
+                        for (int l = 0; l < P.n_lights; ++l) {
+                            v3 wi = mk(0, 0, 0);
+                            float tmax = 0.0f, pdf = 0.0f;
+                            const v3 Lv = light_sample(L.light[l], S.pos, wi, pdf, tmax, rng);
+                            if (pdf == 0.0f) continue;
+                            const float bias = 0.01f;
+                            ++nsh;
+                            const bool vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias);
+                            const float cosv = smax(0.0f, dot(S.ng, wi));
+                            const v3 fr = eval_bxdf(ob);
+                            rad = rad + div3s(((fr * (float)vis) * Lv) * cosv, pdf);
+                        }
+                    }
+                } else {
+                    // NormalIntegrator::integrate (Src/integrator.h:28-37)
+                    if (obj >= 0) rad = normal_color(S.ns);
+                }
+            }
+            // integrate(...) / pdf (pinhole pdf 1) and the invalid-radiance check
+            // (Src/renderer.cpp:53-73), then addPixel in sample order
+            const v3 r = rad / 1.0f;
+            const bool bad = __builtin_isnan(r.x) || __builtin_isnan(r.y) || __builtin_isnan(r.z) ||
+                             __builtin_isinf(r.x) || __builtin_isinf(r.y) || __builtin_isinf(r.z) || r.x < 0.0f ||
+                             r.y < 0.0f || r.z < 0.0f;
+            const uint64_t vm = __ballot(member && !bad);
+            nrej += (uint32_t)(__builtin_popcountll(M) - __builtin_popcountll(vm));
+            if (member && !bad) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(vm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)vm, 0u));
+                sum[rank] = r.x, sum[kPixSumStride + rank] = r.y, sum[2 * kPixSumStride + rank] = r.z;
+            }
+            wave_sync();
+            if (lane < 3) {
+                const f4* q4 = reinterpret_cast<const f4*>(sum + kPixSumStride * lane);
+                const uint32_t nv = (uint32_t)__builtin_popcountll(vm);
+                for (uint32_t j = 0; j < nv; j += 8) {
+                    const f4 a = q4[j / 4], b = q4[j / 4 + 1];
+                    acc = acc + a.x;
+                    if (j + 1 < nv) acc = acc + a.y;
+                    if (j + 2 < nv) acc = acc + a.z;
+                    if (j + 3 < nv) acc = acc + a.w;
+                    if (j + 4 < nv) acc = acc + b.x;
+                    if (j + 5 < nv) acc = acc + b.y;
+                    if (j + 6 < nv) acc = acc + b.z;
+                    if (j + 7 < nv) acc = acc + b.w;
+                }
+            }
+            wave_sync();   // the buffer is rewritten by the next window
+            k += cnt;
+            o += 2u * pos;
+        }
+        if (lane < 3) px[lane] = acc;
+        // the pixel's counters, as the per-slot schedules leave them for k_finish: one
+        // Scene::intersect per sample, its shadow rays and rejects, the stream cursor, and the
+        // twists a std::mt19937 makes to produce x[624 .. o)
+        for (int off = 32; off > 0; off >>= 1) nsh += __shfl_down(nsh, off);
+        if (lane == 0) {
+            P.c_seg[s] = P.spp;
+            P.c_shadow[s] = nsh;
+            P.c_rej[s] = nrej;
+            P.c_stall[s] = 0;
+            P.rng_c[s] = o;
+            P.rng_g[s] = kMT + kMT * ((o - kMT + kMT - 1u) / kMT);
+            P.sample_k[s] = P.spp;
+            P.state[s] = ST_DONE;
+        }
+    }
+}
+
+}  // namespace xrt
+
+#include "launch.h"
+
+namespace xrt {
+
+bool use_pixel(const KParams& P) {
+    return one_hit(P.integrator) && step_lds_bytes(P) != 0 && pix_lds_bytes(P) <= kPixLds;
+}
+
+size_t pix_lds_bytes(const KParams& P) { return pix_wave_off(P) + (size_t)(kPixBlock / 64) * kPixWaveLds; }
+
+template <int SCN, int INTEG>
+static hipError_t pixel_i(const KParams& P, uint32_t* work, hipStream_t st) {
+    const size_t lds = pix_lds_bytes(P);
+    auto kern = k_pixel<SCN, INTEG>;
+    // persistent grid: as many blocks as fit on the device at once (LDS and VGPR bound), at
+    // most one wave per pixel
+    int dev = 0, ncu = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kPixBlock, lds);
+    if (e != hipSuccess) return e;
+    const uint64_t want = ((uint64_t)P.n_slots + kPixBlock / 64 - 1) / (kPixBlock / 64);
+    const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(1, per_cu) * ncu, want));
+    hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(kPixBlock), lds, st, P, work);
+    return hipGetLastError();
+}
+
+template <int SCN>
+static hipError_t pixel_s(const KParams& P, uint32_t* work, hipStream_t st) {
+    if (P.integrator == XRT_INTEGRATOR_DIRECT) return pixel_i<SCN, XRT_INTEGRATOR_DIRECT>(P, work, st);
+    return pixel_i<SCN, XRT_INTEGRATOR_NORMAL>(P, work, st);
+}
+
+hipError_t launch_pixel(const KParams& P, uint32_t* work, hipStream_t st) {
+    if (!use_pixel(P)) return hipErrorInvalidValue;
+    if (hipMemsetAsync(work, 0, sizeof(uint32_t), st) != hipSuccess) return hipErrorInvalidValue;
+    switch (P.scene_kind) {
+        case SCN_TRI: return pixel_s<SCN_TRI>(P, work, st);
+        case SCN_SPHERE: return pixel_s<SCN_SPHERE>(P, work, st);
+        default: return pixel_s<SCN_MIXED>(P, work, st);
+    }
+}
+
+}  // namespace xrt

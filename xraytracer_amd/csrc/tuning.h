@@ -32,6 +32,14 @@
 #define XRT_KSTEP_WAVES XRT_STEP_WAVES   // k_step (C3, C5) alone
 #endif
 
+// ---- pixel-parallel sample chains (k_pixel: Direct / Normal, pixel.hip)
+#ifndef XRT_PIX_BLOCK
+#define XRT_PIX_BLOCK 512    // threads per block (8 waves share one LDS copy of the scene)
+#endif
+#ifndef XRT_PIX_WAVES
+#define XRT_PIX_WAVES 4      // min waves per SIMD (<= 128 VGPRs)
+#endif
+
 // ---- the fused two-level schedule (k_step_merged<..., BVH = true>: C4)
 #ifndef XRT_BVH_WAVES
 #define XRT_BVH_WAVES 4      // 4 waves per SIMD (128 VGPRs, ~30 spilled): C4 -11% vs 3 (no spills), 2: +40%

@@ -131,6 +131,8 @@ constexpr int kSmallTris = 1024;   // scenes up to this size keep every triangle
 constexpr int kLargeObjTris = 256;  // two-level trace: mesh objects above this go into the BVH
 constexpr int kSmallObjs = 256;
 constexpr unsigned kStepLds = 64u * 1024u;   // LDS budget of the fused schedule (k_step)
+constexpr int kStatsWork = 32;               // KParams::stats word k_pixel counts the pixels taken in
+constexpr unsigned kPixLds = 160u * 1024u;   // k_pixel: scene + per-wave stream windows (gfx950: 160 KiB per workgroup)
 
 struct DLight {  // e1/e2/Ng precomputed on the host with the reference constructor's ops
     int kind;

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include "bvh.h"
+#include "lscene.h"
 #include "path_common.h"
 
 // minimum waves per SIMD the wavefront kernels are compiled for (launch bounds; experiment
@@ -215,14 +216,6 @@ __global__ __launch_bounds__(kBlock) void k_trace(KParams P, const uint32_t* __r
 // `t < best` scan over all triangles (Src/scene.cpp:190-200, primitive.cpp:83-131).
 // Shadow rays test occluder triangles only and stop at the first hit (Scene::occluded).
 // One ray per lane; the traversal stack lives in LDS (kBvhStack entries per thread).
-__device__ __forceinline__ bool bvh_box(const f4& mn, const f4& mx, v3 o, v3 inv, float tlim) {
-    const float tx0 = (mn.x - o.x) * inv.x, tx1 = (mx.x - o.x) * inv.x;
-    const float ty0 = (mn.y - o.y) * inv.y, ty1 = (mx.y - o.y) * inv.y;
-    const float tz0 = (mn.z - o.z) * inv.z, tz1 = (mx.z - o.z) * inv.z;
-    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
-    return !(tn > tf);
-}
 
 template <bool ANY>
 __device__ __forceinline__ bool bvh_leaf(const KParams& P, int first, int count, v3 o, v3 d, float tmax, float& bt,
@@ -909,27 +902,6 @@ __device__ float medium_density(const DMedium& M, v3 p) {
     return vdb_interp(M, C, q);
 }
 
-// Component-wise quotients a / b and a / (b, b, b) with one division when the numerators (and
-// denominators) are the same bits — achromatic media and throughputs (C5) — else three; the
-// same IEEE quotients either way.  Bit equality, not ==: +0 and -0 differ in the quotient.
-__device__ __forceinline__ bool same3(v3 a) {
-    return __float_as_uint(a.x) == __float_as_uint(a.y) && __float_as_uint(a.y) == __float_as_uint(a.z);
-}
-__device__ __forceinline__ v3 div3s(v3 a, float b) {
-    if (same3(a)) {
-        const float q = a.x / b;
-        return mk(q, q, q);
-    }
-    return a / b;
-}
-__device__ __forceinline__ v3 div3v(v3 a, v3 b) {
-    if (same3(a) && same3(b)) {
-        const float q = a.x / b.x;
-        return mk(q, q, q);
-    }
-    return a / b;
-}
-
 // Medium::sampleWavelength + DiscreteEmpiricalDistribution1D (Src/medium.h:102-115,
 // Src/sampler.h:53-94).  lower_bound past the end is UB in the reference; clamped to 2.
 __device__ __forceinline__ uint32_t sample_wavelength(v3 thr, v3 albedo, Rng& rng, v3& pmf) {
@@ -1478,195 +1450,6 @@ __global__ __launch_bounds__(kBlock, XRT_SHADE_WAVES) void k_shade(KParams P, co
     (void)req_count;
 }
 
-struct HitRec {
-    float t, u, v;
-    int code;           // winner: (kind << 28) | index, -1 miss
-    int surf, dp;       // mixed scenes: last SurfaceInfo / dpdu writer
-    float st, su, sv, du, dv, t1;
-};
-
-// Sphere scenes (C3): stackless traversal of the threaded BVH (bvh.h SkipNode) in LDS.
-// Same exactness argument as the triangle BVH: boxes are the spheres' bounds padded far
-// beyond the float error of Sphere::intersect's hit point, a box is entered when it
-// overlaps [0, best t] (inclusive), and the closest hit is the lexicographic minimum of
-// (t, original index) — the reference's in-order strict `t < best` scan over the objects
-// (Src/scene.cpp:190-200, primitive.h:106-124).  Any-hit for shadow rays skips spheres of
-// area-light objects (Scene::occluded, Src/scene.cpp:202-211).
-template <bool ANY>
-__device__ __forceinline__ bool sphere_bvh(const LScene& L, v3 o, v3 d, float tmax, float& bt, int& bk) {
-    const v3 inv = rcp3(d);
-    int i = 0;
-    while (i < L.n_snode) {
-        const f4 a = L.snode[2 * i], b = L.snode[2 * i + 1];
-        if (!bvh_box(a, b, o, inv, ANY ? tmax : bt)) {
-            i = __float_as_int(a.w);
-            continue;
-        }
-        const int leaf = __float_as_int(b.w);
-        if (leaf >= 0) {
-            const int first = leaf & 0xffffff, end = first + (leaf >> 24);
-            for (int j = first; j < end; ++j) {
-                const int kw = L.sbk[j];
-                if (ANY && !(kw & (1 << 30))) continue;
-                const f4 S = L.ssph[j];
-                float t;
-                if (!sphere_hit(o, d, xyz(S), S.w, t)) continue;
-                if (ANY) {
-                    if (t < tmax) return true;
-                } else {
-                    const int k = kw & 0x3fffffff;
-                    if (t < bt || (t == bt && k < bk)) bt = t, bk = k;
-                }
-            }
-        }
-        ++i;
-    }
-    return false;
-}
-
-// Scene::intersect over the LDS scene (Src/scene.cpp:190-200)
-template <int SCN>
-__device__ __forceinline__ void closest_l(const KParams& P, const LScene& L, v3 o, v3 d, HitRec& h) {
-    h.t = kINF, h.u = h.v = 0.0f, h.code = -1, h.surf = -1, h.dp = -1, h.t1 = kINF;
-    h.st = h.su = h.sv = h.du = h.dv = 0.0f;
-    if (SCN == SCN_TRI) {
-        const v3 inv = rcp3(d);
-        for (int ob = 0; ob < P.n_objs; ++ob) {
-            const DObjBox B = L.box[ob];
-            const bool ne = box_overlap(o, inv, B, h.t);
-            if (!ne) continue;
-            const int end = B.first + (B.count_occ & 0x7fffffff);
-            for (int k = B.first; k < end; ++k) {
-                float t, u, v;
-                if (ray_tri(o, d, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t, u, v) &&
-                    t < h.t)
-                    h.t = t, h.u = u, h.v = v, h.code = k;
-            }
-        }
-    } else if (SCN == SCN_SPHERE) {
-        if (L.n_snode > 0) {
-            float bt = kINF;
-            int bk = -1;
-            (void)sphere_bvh<false>(L, o, d, kINF, bt, bk);
-            if (bk >= 0) h.t = bt, h.code = (1 << 28) | bk;
-            return;
-        }
-        for (int k = 0; k < P.n_sph; ++k) {
-            const f4 S = L.sph[k];
-            float t;
-            if (sphere_hit(o, d, xyz(S), S.w, t) && t < h.t) h.t = t, h.code = (1 << 28) | k;
-        }
-    } else {
-        for (int sg = 0; sg < P.n_segs; ++sg) {
-            const DSeg seg = P.segs[sg];
-            if (seg.kind == SEG_TRI) {
-                for (int k = seg.first; k < seg.first + seg.count; ++k) {
-                    float t, u, v;
-                    if (ray_tri(o, d, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t, u, v) &&
-                        t < h.t)
-                        h.t = t, h.u = u, h.v = v, h.code = k, h.surf = k, h.st = t, h.su = u, h.sv = v, h.dp = k,
-                        h.du = u, h.dv = v;
-                }
-            } else if (seg.kind == SEG_SPHERE) {
-                for (int k = seg.first; k < seg.first + seg.count; ++k) {
-                    const f4 S = L.sph[k];
-                    float t;
-                    if (sphere_hit(o, d, xyz(S), S.w, t) && t < h.t)
-                        h.t = t, h.u = h.v = 0.0f, h.code = (1 << 28) | k, h.surf = h.code, h.st = t;
-                }
-            } else {
-                for (int b = seg.first; b < seg.first + seg.count; ++b) {
-                    float t0, t1;
-                    if (box_hit(o, d, xyz(L.bx[2 * b]), xyz(L.bx[2 * b + 1]), t0, t1))
-                        h.t = t0, h.t1 = t1, h.code = (2 << 28) | b;
-                }
-            }
-        }
-    }
-}
-
-// Scene::occluded over the LDS scene (Src/scene.cpp:202-211): area-light objects skipped
-template <int SCN>
-__device__ __forceinline__ bool occluded_l(const KParams& P, const LScene& L, v3 o, v3 d, float tmax) {
-    if (SCN == SCN_TRI) {
-        const v3 inv = rcp3(d);
-        for (int ob = 0; ob < P.n_objs; ++ob) {
-            const DObjBox B = L.box[ob];
-            const bool ne = B.count_occ < 0 && box_overlap(o, inv, B, tmax);
-            if (!ne) continue;
-            const int end = B.first + (B.count_occ & 0x7fffffff);
-            for (int k = B.first; k < end; ++k) {
-                float t, u, v;
-                if (ray_tri(o, d, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t, u, v) &&
-                    t < tmax)
-                    return true;
-            }
-        }
-        return false;
-    } else {
-        if (SCN == SCN_SPHERE && L.n_snode > 0) {
-            float bt = kINF;
-            int bk = -1;
-            return sphere_bvh<true>(L, o, d, tmax, bt, bk);
-        }
-        for (int sg = 0; sg < P.n_segs; ++sg) {
-            const DSeg seg = P.segs[sg];
-            if (SCN == SCN_MIXED && seg.kind == SEG_TRI) {
-                for (int k = seg.first; k < seg.first + seg.count; ++k) {
-                    if (L.tri[3 * k + 1].w == 0.0f) continue;
-                    float t, u, v;
-                    if (ray_tri(o, d, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t, u, v) &&
-                        t < tmax)
-                        return true;
-                }
-            } else if (seg.kind == SEG_SPHERE) {
-                for (int k = seg.first; k < seg.first + seg.count; ++k) {
-                    if (!(L.sobj[k] & (1 << 30))) continue;
-                    const f4 S = L.sph[k];
-                    float t;
-                    if (sphere_hit(o, d, xyz(S), S.w, t) && t < tmax) return true;
-                }
-            } else if (SCN == SCN_MIXED && seg.kind == SEG_BOX) {
-                return true;   // BoxMesh::occluded (Src/primitive.h:266-268)
-            }
-        }
-        return false;
-    }
-}
-
-// IntersectInfo::surfaceInfo from a hit record (see surface<>)
-template <int SCN>
-__device__ __forceinline__ int surface_l(const LScene& L, v3 o, v3 d, const HitRec& h, Surf& S) {
-    S.pos = S.ng = S.ns = S.dpdu = S.dpdv = mk(0, 0, 0);
-    if (h.code < 0) return -1;
-    int surf = h.code, dp = (SCN == SCN_TRI) ? h.code : -1;
-    float st = h.t, su = h.u, sv = h.v, du = h.u, dv = h.v;
-    if (SCN == SCN_MIXED) surf = h.surf, dp = h.dp, st = h.st, su = h.su, sv = h.sv, du = h.du, dv = h.dv;
-    if (surf >= 0) {
-        const int kind = surf >> 28, idx = surf & 0x0fffffff;
-        S.pos = ray_at(o, d, st);
-        if (kind == SEG_TRI) {
-            S.ng = xyz(L.tng[idx]);
-            S.ns = tri_ns_l(L, idx, su, sv);
-        } else {
-            S.ng = normalize(ray_at(o, d, st) - xyz(L.sph[idx]));
-            S.ns = S.ng;
-        }
-    }
-    if (dp >= 0) onb(tri_ns_l(L, dp & 0x0fffffff, du, dv), S.dpdu, S.dpdv);
-    const int kind = h.code >> 28, idx = h.code & 0x0fffffff;
-    if (kind == SEG_TRI) return __float_as_int(L.tri[3 * idx].w);
-    if (kind == SEG_SPHERE) return L.sobj[idx] & 0x3fffffff;
-    return __float_as_int(L.bx[2 * idx].w);
-}
-
-// object index of a hit record (see surface_l)
-__device__ __forceinline__ int hit_object(const LScene& L, const HitRec& h) {
-    const int kind = h.code >> 28, idx = h.code & 0x0fffffff;
-    if (kind == SEG_TRI) return __float_as_int(L.tri[3 * idx].w);
-    if (kind == SEG_SPHERE) return L.sobj[idx] & 0x3fffffff;
-    return __float_as_int(L.bx[2 * idx].w);
-}
 
 // VolumePathTracingNEE's light sample at a scattering point (Src/integrator.h:539-560):
 // sampleDirectionToLight (:586-602, Scene::sampleAreaLight Src/scene.cpp:182-188) and
@@ -1740,39 +1523,8 @@ __global__ __launch_bounds__(BS, XRT_KSTEP_WAVES) void k_step(KParams P, const u
                                                   uint32_t visits) {
     extern __shared__ __attribute__((aligned(16))) f4 lds_step[];
     char* lb = reinterpret_cast<char*>(lds_step);
-    const StepLayout Lo = step_layout(P);
-    LScene L;
-    L.tri = reinterpret_cast<const f4*>(lb + Lo.tri);
-    L.tng = reinterpret_cast<const f4*>(lb + Lo.tng);
-    L.nrm = reinterpret_cast<const f4*>(lb + Lo.nrm);
-    L.box = reinterpret_cast<const DObjBox*>(lb + Lo.box);
-    L.sph = reinterpret_cast<const f4*>(lb + Lo.sph);
-    L.bx = reinterpret_cast<const f4*>(lb + Lo.bx);
-    L.obj = reinterpret_cast<const DObj*>(lb + Lo.obj);
-    L.light = reinterpret_cast<const DLight*>(lb + Lo.light);
-    L.sobj = reinterpret_cast<const int*>(lb + Lo.sobj);
     const int tid = threadIdx.x;
-    lds_copy(const_cast<f4*>(L.tri), P.tri, 3 * P.n_tris, tid, BS);
-    lds_copy(const_cast<f4*>(L.tng), P.tri_ng, P.n_tris, tid, BS);
-    lds_copy(const_cast<f4*>(L.nrm), P.tri_nrm, 3 * P.n_tris, tid, BS);
-    if (SCN == SCN_TRI) lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid, BS);
-    lds_copy(const_cast<f4*>(L.bx), P.box, 2 * P.n_box, tid, BS);
-    lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid, BS);
-    if (SCN == SCN_SPHERE && P.n_snode > 0) {
-        // sphere BVH in LDS; per-hit tables read from global memory (step_layout)
-        L.snode = reinterpret_cast<const f4*>(lb + Lo.snode);
-        L.ssph = reinterpret_cast<const f4*>(lb + Lo.ssph);
-        L.sbk = reinterpret_cast<const int*>(lb + Lo.sbk);
-        L.n_snode = P.n_snode;
-        lds_copy(const_cast<f4*>(L.snode), P.snode, 2 * P.n_snode, tid, BS);
-        lds_copy(const_cast<f4*>(L.ssph), P.ssph, P.n_sph, tid, BS);
-        lds_copy(const_cast<int*>(L.sbk), P.sbk, P.n_sph, tid, BS);
-        L.sph = P.sph, L.sobj = P.sph_obj, L.obj = P.objs;
-    } else {
-        lds_copy(const_cast<f4*>(L.sph), P.sph, P.n_sph, tid, BS);
-        lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid, BS);
-        lds_copy(const_cast<int*>(L.sobj), P.sph_obj, P.n_sph, tid, BS);
-    }
+    const LScene L = load_lscene(P, lb, tid, BS);
     __syncthreads();
     zero_parts(P, zero_count);
     const int lane = tid & 63;
@@ -2038,9 +1790,9 @@ __global__ __launch_bounds__(BS, XRT_KSTEP_WAVES) void k_step(KParams P, const u
         // live list of the next round (partitioned, one atomic per wave), then the wave's
         // refills in-line (as k_step_merged: no k_refill launch between step launches)
         wave_append(!(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
-        if constexpr (XRT_KSTEP_LDS_REFILL == 1 || (XRT_KSTEP_LDS_REFILL == 2 && SCN != SCN_SPHERE)) {
-            __shared__ __attribute__((aligned(16))) uint32_t rbuf[BS / 64][kMT];   // wave_refill staging
-            wave_refill(P, want_req, s, g, lane, rbuf[tid >> 6]);
+        if (kstep_refill_off(P, BS)) {   // wave_refill staging: the wave's kMT words after the scene
+            uint32_t* rbuf = reinterpret_cast<uint32_t*>(lb + kstep_refill_off(P, BS)) + (tid >> 6) * kMT;
+            wave_refill(P, want_req, s, g, lane, rbuf);
         } else {
             // sphere-BVH scenes: twisted from global memory (L2), no LDS buffer beside the
             // scene's ~45 KB (3 blocks per CU instead of 2)
@@ -2641,11 +2393,19 @@ size_t step_lds_bytes(const KParams& P) {
     return total <= kStepLds ? (total + 15) / 16 * 16 : 0;
 }
 
+// k_step's dynamic LDS: the scene carve, plus each wave's refill staging buffer where the
+// in-line refill is staged through LDS (kstep_refill_off).  The staging sits outside the
+// kStepLds scene budget (at most 64 KiB + 10 KiB per 256-thread block, within gfx950's
+// 160 KiB per workgroup).
+static size_t kstep_lds_bytes(const KParams& P, int bs) {
+    const size_t off = kstep_refill_off(P, bs);
+    return off ? off + (size_t)(bs / 64) * kMT * 4 : step_lds_bytes(P);
+}
+
 template <int SCN>
 static hipError_t step_i(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
                          uint32_t* out_count, uint32_t* zero, uint32_t* req_count, uint32_t visits, uint32_t blocks,
                          hipStream_t st) {
-    const size_t lds = step_lds_bytes(P);
     // Sphere-BVH scenes (C3) keep ~45 KB of BVH and spheres in LDS, so 256-thread blocks stop
     // at 3 per CU (3 waves per SIMD); 512-thread blocks share one copy between 8 waves
     // (4 waves per SIMD, the VGPR limit).  Same partitions, same results.
@@ -2654,9 +2414,10 @@ static hipError_t step_i(const KParams& P, const uint32_t* list, const uint32_t*
         // and chunk b / n_part of gridDim / n_part chunks)
         const uint32_t chunks = std::max(1u, blocks / P.n_part);
         hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_DIRECT, 512>), dim3(P.n_part * ((chunks + 1) / 2)), dim3(512),
-                           lds, st, P, list, count, out, out_count, zero, req_count, visits);
+                           kstep_lds_bytes(P, 512), st, P, list, count, out, out_count, zero, req_count, visits);
         return hipGetLastError();
     }
+    const size_t lds = kstep_lds_bytes(P, kBlock);
     if (P.integrator == XRT_INTEGRATOR_DIRECT)
         hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_DIRECT>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
                            out, out_count, zero, req_count, visits);

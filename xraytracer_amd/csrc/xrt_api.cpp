@@ -806,6 +806,9 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     // scene through LDS tiles; k_shade refills its slots' rings in-line).
     // Two-level scenes (C4) take the merged kernel with the wave's own BVH walk.
     const bool bvh = !(p->flags & (XRT_FLAG_WAVEFRONT | XRT_FLAG_NO_MERGED)) && use_step_bvh(P);
+    // Direct / Normal over an LDS-resident scene: pixel-parallel sample chains (pixel.hip) —
+    // one k_pixel launch between k_seed and k_finish, no live lists, no refill launch
+    const bool pixel = !bvh && !(p->flags & (XRT_FLAG_WAVEFRONT | XRT_FLAG_NO_PIXEL)) && use_pixel(P);
     const bool fused = bvh || (!(p->flags & XRT_FLAG_WAVEFRONT) && step_lds_bytes(P) != 0);
     const bool merged = bvh || (fused && !(p->flags & XRT_FLAG_NO_MERGED) && use_step_merged(P));
     // live-list partitions (a multiple of the 8 XCDs): every wave appends to its partition's
@@ -874,6 +877,13 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
         HIPCHK(c, hipMemcpyAsync(fb, h_out, npix * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(P.stats, 0, 512, c->stream));
     HIPCHK(c, launch(XRT_K_SEED, [&] { return launch_seed(P, lists[0], counts_at(0), counts_at(1), req_counts, c->stream); }));
+    if (pixel) {
+        // every pixel of the shard in one persistent launch; the pixel counter is a stats word
+        // (zeroed with them above)
+        uint32_t* work = reinterpret_cast<uint32_t*>(P.stats + kStatsWork);
+        hipError_t e = launch(XRT_K_STEP, [&] { return launch_pixel(P, work, c->stream); });
+        if (e != hipSuccess) return hip_err(c, e, "k_pixel");
+    }
     // refill epochs: shading launches of epoch e append to req_counts[e & 1]; k_refill(e)
     // consumes it and clears req_counts[(e + 1) & 1] for epoch e + 1.  Epoch 0 is the
     // first twist of every slot, requested by k_seed.
@@ -888,7 +898,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             return launch_refill(P, req_counts + a * kMaxParts, req_counts + b * kMaxParts, c->stream);
         });
     };
-    HIPCHK(c, refill());
+    if (!pixel) HIPCHK(c, refill());
 
     const uint32_t blocks = P.n_part * ((P.part_cap + 255) / 256);   // one entry per thread
     // GI/Direct: at most max_depth + 1 shade passes per sample; VPT walks are unbounded
@@ -903,7 +913,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     hipEvent_t* poll_ev = c->poll_ev;
     uint64_t it = 0;
     int poll_slot = 0;
-    bool done = false;
+    bool done = pixel;   // the pixel schedule has no step loop
     // k_step rotates three live counters: round i reads counts[i%3], appends to
     // counts[(i+1)%3] and clears counts[(i+2)%3] for round i+1 (every step kernel twists its
     // slots' rings in-line at the end of the launch: no k_refill after the seeding one).
@@ -924,7 +934,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     P.rng_keep = merged                      ? step_visits * step_merged_draws(P) + step_merged_draws(P)
                  : (volumetric && kVptEvents) ? step_visits * kVptEventDraws + kRngVisit
                                               : step_visits * kVisitDraws + kRngVisit;
-    if (P.rng_keep > kMT) return set_err(c, XRT_ERR_INVALID, "visits_per_launch too large for the RNG ring");
+    if (!pixel && P.rng_keep > kMT) return set_err(c, XRT_ERR_INVALID, "visits_per_launch too large for the RNG ring");
     // device copy of the (now final) parameters for kernels that read them from memory
     if ((rc = ensure(c, c->kparams, sizeof(KParams)))) return rc;
     HIPCHK(c, hipMemcpyAsync(c->kparams.p, &P, sizeof(KParams), hipMemcpyHostToDevice, c->stream));
@@ -1025,13 +1035,14 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
                      " in-wave walks %llu\n", hs[38], hs[39], hs[37], hs[36], hs[35]);
     S.segments = hs[0], S.shadow_rays = hs[1], S.draws = hs[2], S.rejected = hs[3], S.stalled = hs[4];
     S.rng_twists = hs[7];
-    S.schedule = !fused ? XRT_SCHED_WAVEFRONT
+    S.schedule = pixel   ? XRT_SCHED_PIXEL
+                 : !fused ? XRT_SCHED_WAVEFRONT
                  : bvh    ? XRT_SCHED_STEP_BVH
                  : merged ? XRT_SCHED_STEP_MERGED
                  : use_step_tri(P) ? XRT_SCHED_STEP_TRI : XRT_SCHED_STEP;
     S.partitions = P.n_part;
-    if (fused) S.visits_per_launch = step_visits;
-    if (merged) {
+    if (fused && !pixel) S.visits_per_launch = step_visits;
+    if (merged && !pixel) {
         S.slots_per_wave = step_merged_spw(P, n);   // the layout of the first launch (every launch's: layout_launches)
         S.group_lanes = step_merged_group(P, S.slots_per_wave);
     }

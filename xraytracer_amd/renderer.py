@@ -70,15 +70,17 @@ class HipRenderer:
                max_depth=None, schedule="auto", slots_per_wave=0, visits_per_launch=0, group=True,
                accumulate=False, deep="auto"):
         """schedule: "auto" (fused k_step when the scene fits in LDS — for small triangle
-        scenes with merged shadow + extension traces — else the multi-pass wavefront),
-        "wavefront" (always k_shade + k_trace) or "step_tri" (fused, one cooperative trace
-        per ray kind instead of the merged traces).  slots_per_wave / visits_per_launch /
+        scenes with merged shadow + extension traces, for Direct / Normal pixel-parallel
+        sample chains (k_pixel) — else the multi-pass wavefront), "step" (the per-slot fused
+        schedule also for Direct / Normal), "wavefront" (always k_shade + k_trace) or
+        "step_tri" (per-slot fused, one cooperative trace per ray kind instead of the merged
+        traces).  slots_per_wave / visits_per_launch /
         group fix the merged schedule's launch geometry (0 / True = the library's choice);
         results never depend on them.  accumulate: add the samples to the output buffer's
         current contents before the divide (XRT_FLAG_ACCUMULATE, Renderer::render's contract).
         deep: the two-level trace's BVH walk, "auto", "single" (one lane per queued ray) or
         "quad" (four); results never depend on it."""
-        if schedule not in ("auto", "wavefront", "step_tri"):
+        if schedule not in ("auto", "step", "wavefront", "step_tri"):
             raise ValueError(f"unknown schedule {schedule!r}")
         if deep not in ("auto", "single", "quad"):
             raise ValueError(f"unknown deep walk {deep!r}")
@@ -89,6 +91,7 @@ class HipRenderer:
         p.shard_index, p.shard_count = shard_index, shard_count
         p.flags = ((abi.XRT_FLAG_TIMING if timing else 0) | (abi.XRT_FLAG_WAVEFRONT if schedule == "wavefront" else 0) |
                    (abi.XRT_FLAG_NO_MERGED if schedule == "step_tri" else 0) | (0 if group else abi.XRT_FLAG_NO_GROUP) |
+                   (abi.XRT_FLAG_NO_PIXEL if schedule in ("step", "step_tri") else 0) |
                    (abi.XRT_FLAG_ACCUMULATE if accumulate else 0) |
                    {"auto": 0, "single": abi.XRT_FLAG_DEEP_SINGLE, "quad": abi.XRT_FLAG_DEEP_QUAD}[deep])
         p.slots_per_wave, p.visits_per_launch = slots_per_wave, visits_per_launch
