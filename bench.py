@@ -178,7 +178,15 @@ def main():
     import numpy as np
     import torch
 
-    action, what = plan_launch(args.gpus, os.environ, torch.cuda.device_count())
+    # Tests only (tests/test_bench_launch.py): XRT_BENCH_STANDIN="module:factory" swaps the
+    # HIP renderer for a CPU stand-in (not the oracle) so the multi-rank plumbing — the spawn,
+    # torch.distributed.run's rank environment, process-group init, the framebuffer reduce and
+    # the max-over-ranks timing — runs end to end on a GPU-less machine over gloo.  Read before
+    # any GPU call; the default run never sets it, and a stand-in line says so in "data".
+    standin = os.environ.get("XRT_BENCH_STANDIN")
+    on_gpu = not standin
+    devices = torch.cuda.device_count() if on_gpu else env_int("XRT_BENCH_STANDIN_DEVICES", 8)
+    action, what = plan_launch(args.gpus, os.environ, devices)
     if action == "error":
         print(f"bench.py: {what}", file=sys.stderr, flush=True)
         sys.exit(2)
@@ -193,24 +201,40 @@ def main():
     local = env_int("LOCAL_RANK", 0)
     dist = None
     if world > 1:
+        import datetime
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
+        # an explicit collective timeout: a rank that never arrives ends the job instead of
+        # hanging it (XRT_DIST_TIMEOUT_S, default 10 minutes)
+        timeout = datetime.timedelta(seconds=env_int("XRT_DIST_TIMEOUT_S", 600))
+        if on_gpu:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
+        else:
+            dist.init_process_group("gloo", timeout=timeout)
+    elif on_gpu:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local) if on_gpu else torch.device("cpu")
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
 
     cfg = dict(scenes.CONFIGS[args.config])
     if args.spp:
         cfg["spp"] = args.spp
     W, H, SPP = cfg["width"], cfg["height"], cfg["spp"]
     scene = scenes.build(args.config)
-    r = HipRenderer(SPP, device=local)
+    if standin:
+        import importlib
+        mod, fn = standin.split(":")
+        r = getattr(importlib.import_module(mod), fn)(SPP, local)
+    else:
+        r = HipRenderer(SPP, device=local)
     r.upload(scene)
     fb = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
     timing = not args.no_timing
 
-    sharded = distributed.ShardedRenderer(r, dist)
+    sharded = distributed.ShardedRenderer(r, dist, time_reduce=True)
 
     def step(timed):
         # rank's rows, then reduce(SUM) into rank 0; the render waits for the work queued on
@@ -219,10 +243,10 @@ def main():
 
     for _ in range(args.warmup):
         step(False)
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     agg = {k: 0.0 for k in ("segments", "shadow_rays", "draws", "samples", "iterations", "rejected")}
     kms = np.zeros(abi.XRT_K_COUNT)
@@ -236,10 +260,10 @@ def main():
         kms += np.array(list(st.kernel_ms))
         sched = int(st.schedule)
         kl += np.array(list(st.launches))
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     if dist is not None:
         elapsed = distributed.max_over_ranks(elapsed, dist, device=dev)
@@ -329,7 +353,8 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic" if on_gpu else f"STAND-IN renderer {standin} (plumbing test, not a measurement)",
             "config": {"workload": f"{args.config}: {cfg['scene']} {W}x{H}, {SPP} spp, {cfg['integrator']}"
                                    f"(maxDepth={cfg['max_depth']})",
                        "width": W, "height": H, "spp": SPP, "integrator": cfg["integrator"],

@@ -33,13 +33,19 @@ def main():
     d = args[0]
     pat = args[1] if len(args) > 1 else "k_step"
     st = glob.glob(os.path.join(d, "kt", "*kernel_stats.csv"))
+    # the kernel family's average launch: every dispatch of every instantiation whose name
+    # matches (e.g. k_step_merged's 64-, 32- and 16-slot layouts), total time / total calls
     avg_ns = None
+    fam_ns, fam_calls = 0.0, 0
     if st:
         for r in csv.DictReader(open(st[0])):
             print(f'{float(r["TotalDurationNs"]) / 1e6:9.3f} ms {int(r["Calls"]):6d} calls '
                   f'avg {float(r["AverageNs"]) / 1e3:9.2f} us  {r["Name"][:80]}')
-            if pat in r["Name"] and avg_ns is None:
-                avg_ns = float(r["AverageNs"])
+            if pat in r["Name"]:
+                fam_ns += float(r["TotalDurationNs"])
+                fam_calls += int(r["Calls"])
+        if fam_calls:
+            avg_ns = fam_ns / fam_calls
     acc = collections.defaultdict(float)
     n = collections.Counter()
     kname = None
@@ -77,7 +83,8 @@ def main():
         out = {"config": traffic[0], "kernel": kname, "launches": launches,
                "fetch_bytes_per_launch": fetch / launches, "write_bytes_per_launch": write / launches,
                "hbm_bytes_per_launch": (fetch + write) / launches,
-               "avg_launch_us_rocprof": avg_ns / 1e3 if avg_ns else None, "source": os.path.basename(d.rstrip("/")),
+               "avg_launch_us_rocprof": avg_ns / 1e3 if avg_ns else None, "rocprof_calls": fam_calls,
+               "rocprof_total_ms": fam_ns / 1e6, "source": os.path.basename(d.rstrip("/")),
                "note": "FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md HBM section; separate --pmc passes"}
         json.dump(out, open(traffic[1], "w"), indent=1)
         print("wrote", traffic[1], out)
@@ -85,7 +92,8 @@ def main():
         launches = n["SQ_INSTS_VALU"]
         out = {"config": pmc_out[0], "kernel": kname, "launches": launches,
                "SQ_INSTS_VALU_per_launch": a["SQ_INSTS_VALU"] / launches,
-               "avg_launch_us_rocprof": avg_ns / 1e3 if avg_ns else None,
+               "avg_launch_us_rocprof": avg_ns / 1e3 if avg_ns else None, "rocprof_calls": fam_calls,
+               "rocprof_total_ms": fam_ns / 1e6,
                "source": os.path.basename(d.rstrip("/"))}
         for k in ("SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_BRANCH",
                   "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_ANY"):

@@ -40,7 +40,9 @@ bool use_pixel(const KParams& P);
 size_t pix_lds_bytes(const KParams& P);
 hipError_t launch_pixel(const KParams& P, uint32_t* work, hipStream_t st);
 // up to `visits` path segments per live slot; appends survivors to out (partitioned
-// counters out_count), low-RNG slots to P.req (req_count); clears zero (next-next round)
+// counters out_count); twists the rings of slots that ran low in-line; clears zero
+// (next-next round).  req_count is unused by the step kernels (kept in the signature of
+// every schedule's step launch; only the seeding k_refill reads the request list)
 // dP: device copy of P (the triangle-scene kernel reads its parameters from memory)
 hipError_t launch_step(const KParams& P, const KParams* dP, const uint32_t* list, const uint32_t* count, uint32_t* out,
                        uint32_t* out_count, uint32_t* zero, uint32_t* req_count, uint32_t visits, uint32_t blocks,

@@ -206,6 +206,116 @@ __device__ __forceinline__ int hit_object(const LScene& L, const HitRec& h) {
     return __float_as_int(L.bx[2 * idx].w);
 }
 
+// ---- packet traversal (k_pixel) ----
+// The rays of a k_pixel wave are coherent: 64 camera rays through one pixel, and their shadow
+// rays toward one light.  These forms walk the scene once per wave at a wave-uniform position
+// (node / object index in SGPRs, node words broadcast from LDS, loop control in SALU) and
+// enter a node when any active lane's segment overlaps it; a lane tests a leaf's primitives
+// only when its own segment overlaps the leaf's box.  A lane that does not overlap a node does
+// not overlap any node below it (children's padded boxes lie inside the parent's), so each
+// lane tests exactly the primitives, in exactly the order, of its own per-lane walk
+// (sphere_bvh / closest_l / occluded_l): same hits, same ties.  Every lane of the wave must
+// call them (ballots); `active` says which lanes have a ray.
+__device__ __forceinline__ int wave_uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+template <bool ANY>
+__device__ __forceinline__ bool sphere_bvh_wave(const LScene& L, v3 o, v3 d, float tmax, float& bt, int& bk,
+                                                bool active) {
+    const v3 inv = rcp3(d);
+    bool occ = false;
+    int i = 0;
+    while (i < L.n_snode) {
+        const f4 a = L.snode[2 * i], b = L.snode[2 * i + 1];
+        const bool ov = active && !occ && bvh_box(a, b, o, inv, ANY ? tmax : bt);
+        if (__ballot(ov) == 0ull) {
+            i = wave_uniform(__float_as_int(a.w));
+            continue;
+        }
+        const int leaf = wave_uniform(__float_as_int(b.w));
+        if (leaf >= 0) {
+            const int first = leaf & 0xffffff, end = first + (leaf >> 24);
+            for (int j = first; j < end; ++j) {
+                const int kw = wave_uniform(L.sbk[j]);
+                if (ANY && !(kw & (1 << 30))) continue;
+                const f4 S = L.ssph[j];
+                float t;
+                if (ov && sphere_hit(o, d, xyz(S), S.w, t)) {
+                    if (ANY) {
+                        if (t < tmax) occ = true;
+                    } else {
+                        const int k = kw & 0x3fffffff;
+                        if (t < bt || (t == bt && k < bk)) bt = t, bk = k;
+                    }
+                }
+            }
+            if (ANY && __ballot(active && !occ) == 0ull) return occ;
+        }
+        ++i;
+    }
+    return occ;
+}
+
+// Scene::intersect for a coherent wave (closest_l's result for every active lane)
+template <int SCN>
+__device__ __forceinline__ void closest_w(const KParams& P, const LScene& L, v3 o, v3 d, HitRec& h, bool active) {
+    if (SCN == SCN_SPHERE && L.n_snode > 0) {
+        h.t = kINF, h.u = h.v = 0.0f, h.code = -1, h.surf = -1, h.dp = -1, h.t1 = kINF;
+        h.st = h.su = h.sv = h.du = h.dv = 0.0f;
+        float bt = kINF;
+        int bk = -1;
+        (void)sphere_bvh_wave<false>(L, o, d, kINF, bt, bk, active);
+        if (bk >= 0) h.t = bt, h.code = (1 << 28) | bk;
+    } else if (SCN == SCN_TRI) {
+        h.t = kINF, h.u = h.v = 0.0f, h.code = -1, h.surf = -1, h.dp = -1, h.t1 = kINF;
+        h.st = h.su = h.sv = h.du = h.dv = 0.0f;
+        const v3 inv = rcp3(d);
+        for (int ob = 0; ob < P.n_objs; ++ob) {
+            const DObjBox B = L.box[ob];
+            const bool ne = active && box_overlap(o, inv, B, h.t);
+            if (__ballot(ne) == 0ull) continue;
+            const int first = wave_uniform(B.first), end = first + wave_uniform(B.count_occ & 0x7fffffff);
+            for (int k = first; k < end; ++k) {
+                float t, u, v;
+                if (ne && ray_tri(o, d, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t, u, v) &&
+                    t < h.t)
+                    h.t = t, h.u = u, h.v = v, h.code = k;
+            }
+        }
+    } else {
+        if (active) closest_l<SCN>(P, L, o, d, h);
+    }
+}
+
+// Scene::occluded for a coherent wave (occluded_l's result for every active lane)
+template <int SCN>
+__device__ __forceinline__ bool occluded_w(const KParams& P, const LScene& L, v3 o, v3 d, float tmax, bool active) {
+    if (SCN == SCN_SPHERE && L.n_snode > 0) {
+        float bt = kINF;
+        int bk = -1;
+        return sphere_bvh_wave<true>(L, o, d, tmax, bt, bk, active);
+    } else if (SCN == SCN_TRI) {
+        const v3 inv = rcp3(d);
+        bool occ = false;
+        for (int ob = 0; ob < P.n_objs; ++ob) {
+            const DObjBox B = L.box[ob];
+            const bool ne = active && !occ && B.count_occ < 0 && box_overlap(o, inv, B, tmax);
+            if (__ballot(ne) == 0ull) continue;
+            const int first = wave_uniform(B.first), end = first + wave_uniform(B.count_occ & 0x7fffffff);
+            for (int k = first; k < end; ++k) {
+                float t, u, v;
+                if (ne && !occ && ray_tri(o, d, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t, u, v) &&
+                    t < tmax)
+                    occ = true;
+            }
+        }
+        return occ;
+    } else {
+        bool occ = false;
+        if (active) occ = occluded_l<SCN>(P, L, o, d, tmax);
+        return occ;
+    }
+}
+
 // k_step's in-line refill staging (wave_refill through LDS, one kMT-word buffer per wave)
 // sits in the dynamic LDS right after the scene carve; returns its byte offset, or 0 where
 // the refill twists from L2 instead (XRT_KSTEP_LDS_REFILL: sphere scenes keep their blocks

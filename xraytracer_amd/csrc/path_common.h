@@ -115,7 +115,13 @@ __device__ inline void wave_twist(uint32_t* ring, uint32_t g, int lane) {
     }
 }
 
-// In-kernel refill for the RNG self-test: every lane with `need` gets its next block.
+// In-line refill from global memory (no LDS buffer): every lane with `need` gets its slot's
+// next block, twisted by the whole wave (wave_twist).  Used by the RNG self-test and by
+// k_step on sphere-BVH scenes (XRT_KSTEP_LDS_REFILL = 2, whose LDS holds the BVH).
+// Invariants: a slot asks only when fewer than rng_keep <= kMT words are left, so the new
+// block x[g, g + 624) overwrites only words the slot has drawn (the other ring half), and
+// reads only the old half, which no lane writes; the workgroup fence orders the stores before
+// the launch ends, and the next reader of the ring is a later kernel launch.
 // Must be called by every lane of the wave (wave-uniform control flow).
 __device__ inline void wave_refill(bool need, uint32_t slot, uint32_t& g, uint32_t* rings, int lane) {
     uint64_t m = __ballot(need);
@@ -636,7 +642,8 @@ __device__ __forceinline__ v3 normal_color(v3 ns) {
 // larger scenes use the multi-pass wavefront (k_shade / k_trace with LDS tiles).  A slot
 // stops early when its RNG ring runs low or it is done; at the end of the launch the slot
 // is appended to the next round's live list and, when fewer than rng_keep words are left,
-// to the refill list k_refill services between rounds.
+// its wave twists the slot's next block in-line (wave_refill) — only the seeding twist of
+// every slot is a k_refill launch.
 struct LScene {
     const f4* tri;      // 3 per triangle
     const f4* tng;      // geometric normal per triangle

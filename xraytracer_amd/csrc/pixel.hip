@@ -47,6 +47,8 @@ constexpr int kPixBlock = XRT_PIX_BLOCK;           // threads per block: 8 waves
 constexpr uint32_t kPixSumStride = 68;             // ordered-sum buffer row (floats): 64 + 4, rows on other banks
 constexpr uint32_t kPixWaveLds = (kMT + 3 * kPixSumStride) * 4;   // per wave: stream window + sum buffer
 
+constexpr bool kPixPacket = XRT_PIX_PACKET != 0;   // wave-uniform scene walks (lscene.h closest_w)
+
 // the words generated per chunk: one pair per lane
 constexpr uint32_t kPixChunk = 128;
 
@@ -140,10 +142,15 @@ __global__ __launch_bounds__(kPixBlock, XRT_PIX_WAVES) void k_pixel(KParams P, u
                 const float u = div_w(P, (float)(int)col + rng.next());
                 const float v = div_h(P, (float)(int)row + rng.next());
                 camera_ray(P, u, v, ro, rd);
+            }
+            {
                 HitRec h;
-                closest_l<SCN>(P, L, ro, rd, h);
-                obj = surface_l<SCN>(L, ro, rd, h, S);
-                kind = obj < 0 ? 0 : (L.obj[obj].light >= 0 ? 1 : 2);
+                if (kPixPacket) closest_w<SCN>(P, L, ro, rd, h, cand);
+                else if (cand) closest_l<SCN>(P, L, ro, rd, h);
+                if (cand) {
+                    obj = surface_l<SCN>(L, ro, rd, h, S);
+                    kind = obj < 0 ? 0 : (L.obj[obj].light >= 0 ? 1 : 2);
+                }
             }
             // the chain through the window (scalar): from candidate 0 (the next sample), a
             // sample at candidate q moves to q + 1, or to q + 1 + NLD after a surface hit
@@ -165,32 +172,30 @@ __global__ __launch_bounds__(kPixBlock, XRT_PIX_WAVES) void k_pixel(KParams P, u
             }
             const bool member = (M >> lane) & 1ull;
             v3 rad = mk(0, 0, 0);
-            if (member) {
-                if (INTEG == XRT_INTEGRATOR_DIRECT) {
-                    // DirectIntegrator::integrate (Src/integrator.h:82-119)
-                    if (kind == 0) {
-                        rad = mk((float)0.18, (float)0.18, (float)0.18);
-                    } else if (kind == 1) {
-                        rad = light_Le(L.light[L.obj[obj].light], S.ns, rd);
-                    } else {
-                        const DObj& ob = L.obj[obj];
-                        for (int l = 0; l < P.n_lights; ++l) {
-                            v3 wi = mk(0, 0, 0);
-                            float tmax = 0.0f, pdf = 0.0f;
-                            const v3 Lv = light_sample(L.light[l], S.pos, wi, pdf, tmax, rng);
-                            if (pdf == 0.0f) continue;
-                            const float bias = 0.01f;
-                            ++nsh;
-                            const bool vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias);
-                            const float cosv = smax(0.0f, dot(S.ng, wi));
-                            const v3 fr = eval_bxdf(ob);
-                            rad = rad + div3s(((fr * (float)vis) * Lv) * cosv, pdf);
-                        }
+            if (INTEG == XRT_INTEGRATOR_DIRECT) {
+                // DirectIntegrator::integrate (Src/integrator.h:82-119); the light loop runs on
+                // every lane (the shadow trace is a wave walk), shading where a sample hit a surface
+                const bool shade = member && kind == 2;
+                if (member && kind == 0) rad = mk((float)0.18, (float)0.18, (float)0.18);
+                if (member && kind == 1) rad = light_Le(L.light[L.obj[obj].light], S.ns, rd);
+                for (int l = 0; l < P.n_lights; ++l) {
+                    v3 wi = mk(0, 0, 0), Lv = mk(0, 0, 0);
+                    float tmax = 0.0f, pdf = 0.0f;
+                    if (shade) Lv = light_sample(L.light[l], S.pos, wi, pdf, tmax, rng);
+                    const bool ray = shade && pdf != 0.0f;
+                    const float bias = 0.01f;
+                    nsh += ray ? 1u : 0u;
+                    bool vis = true;
+                    if (kPixPacket) vis = !occluded_w<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias, ray);
+                    else if (ray) vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias);
+                    if (ray) {
+                        const float cosv = smax(0.0f, dot(S.ng, wi));
+                        const v3 fr = eval_bxdf(L.obj[obj]);
+                        rad = rad + div3s(((fr * (float)vis) * Lv) * cosv, pdf);
                     }
-                } else {
-                    // NormalIntegrator::integrate (Src/integrator.h:28-37)
-                    if (obj >= 0) rad = normal_color(S.ns);
                 }
+            } else if (member && obj >= 0) {
+                rad = normal_color(S.ns);   // NormalIntegrator::integrate (Src/integrator.h:28-37)
             }
             // integrate(...) / pdf (pinhole pdf 1) and the invalid-radiance check
             // (Src/renderer.cpp:53-73), then addPixel in sample order

@@ -378,46 +378,9 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const D
 // triangle whose padded box overlaps [0, best t] is tested by some lane) — the same
 // lexicographic minimum over every triangle the reference's linear scan tests
 // (Src/scene.cpp:190-211, Src/primitive.cpp:83-168).
-
-// One leaf's triangles (BVH leaf order, KParams::bvh_tri: e1.w = occluder, e2.w = original
-// index) against a ray: closest hit as the (t, original index) minimum, or any occluder hit
-// below tmax.  The loads of the whole leaf are issued before the first test.  Mesh::
-// rayTriangleIntersect's decisions via ray_tri_nb (two-level scenes are det_bounded).
 constexpr int kQs = 64;          // quad stack entries (circular; >= kBvh4Stack)
 constexpr int kQsMask = kQs - 1;
 static_assert(kQs >= kBvh4Stack, "quad stacks");
-template <bool ANY>
-__device__ __forceinline__ bool deep_leaf(const KParams& P, int first, int count, v3 o, v3 d, float tmax, float& bt,
-                                          int& bk) {
-    constexpr int B = XRT_DEEP_LEAF_BATCH;
-    static_assert(kBvhLeafTri % B == 0, "leaf batches");
-    bool occ = false;
-#pragma unroll
-    for (int q0 = 0; q0 < (int)kBvhLeafTri; q0 += B) {
-        if (q0 >= count) break;
-        f4 T[B][3];
-#pragma unroll
-        for (int q = 0; q < B; ++q)
-            if (q0 + q < count) {
-                const size_t i = 3 * (size_t)(first + q0 + q);
-                T[q][0] = ldg4(P.bvh_tri, i), T[q][1] = ldg4(P.bvh_tri, i + 1), T[q][2] = ldg4(P.bvh_tri, i + 2);
-            }
-#pragma unroll
-        for (int q = 0; q < B; ++q) {
-            if (q0 + q >= count) break;
-            if (ANY && T[q][1].w == 0.0f) continue;   // area-light objects never occlude
-            float t;
-            if (!ray_tri_nb(o, d, xyz(T[q][0]), xyz(T[q][1]), xyz(T[q][2]), t)) continue;
-            if (ANY) {
-                occ |= t < tmax;
-            } else {
-                const int k = __float_as_int(T[q][2].w);
-                if (t < bt || (t == bt && k < bk)) bt = t, bk = k;
-            }
-        }
-    }
-    return occ;
-}
 
 // The walk of n_deep ranked rays ray_o / ray_d (w: tmax resp. the ray id q * 64 + lane; q = 0:
 // extension ray, closest hit from the key best[lane]; 1 + l: shadow ray l, occlusion bit l of
@@ -430,29 +393,18 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
     constexpr uint64_t kLeads = 0x1111111111111111ull;   // lane 0 of every quad
     const int c = lane & 3;
     SE* qs = stk + (lane >> 2);
-    uint32_t* mbox = reinterpret_cast<uint32_t*>(stk + 16 * kQs);   // steals: (pool entry << 16) | node
-    (void)mbox;
     uint32_t next = 0;   // wave-uniform: first ray not yet taken
     bool active = false, any = false;
-    uint32_t id = 0, ridx = 0;   // the ray's id and its pool entry
-    (void)ridx;
+    uint32_t id = 0;   // the ray's id
     int node = 0, sp = 0, base = 0, bk = -1;   // stack entries [base, sp), circular (kQs)
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0), inv = mk(0, 0, 0);
     float tmax = 0.0f, bt = kINF;
-#if XRT_DEEP_EARLY
-    bool have_next = false;   // nlo / nhi hold child c of `node` (fetched during the last step)
-    f4 nlo = make_float4(0, 0, 0, 0), nhi = nlo;
-#endif
-#ifdef XRT_EXPERIMENTS
-    uint32_t niter = 0, nsteps = 0;
-#endif
     while (true) {
         if (next < n_deep) {
             const uint64_t idle = __ballot(!active) & kLeads;
             if (idle) {
                 const uint32_t idx = next + (uint32_t)__popcll(idle & ((1ull << (lane & ~3)) - 1ull));
                 if (!active && idx < n_deep) {
-                    ridx = idx;
                     const f4 A = ray_o[idx], D = ray_d[idx];
                     id = __float_as_uint(D.w);
                     any = id >= 64u;
@@ -465,67 +417,18 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
                     inv = rcp3(d);
                     node = 0, sp = 0, base = 0;
                     active = true;
-#if XRT_DEEP_EARLY
-                    have_next = false;
-#endif
                 }
                 next += (uint32_t)__popcll(idle);
             }
         }
-#if XRT_DEEP_STEAL
-        // Work stealing once the pool is drained: an idle quad takes the oldest stacked node of
-        // an active ray (the bottom of its stack: the largest pending subtree) and walks that
-        // subtree for the same ray; every quad working on a ray merges into its records (key
-        // minimum, occlusion or) and prunes with the ray's best key so far.  Which quad tests
-        // a triangle does not change the (t, index) minimum nor the occlusion.
-        if (next >= n_deep) {
-            const uint64_t idle = __ballot(!active) & kLeads;
-            const uint64_t vict = __ballot(active && sp - base >= 1) & kLeads;
-            if (idle && vict) {
-                const uint32_t pairs = min((uint32_t)__popcll(idle), (uint32_t)__popcll(vict));
-                const uint64_t below = (1ull << (lane & ~3)) - 1ull;
-                const bool victim = active && sp - base >= 1 && (uint32_t)__popcll(vict & below) < pairs;
-                if (victim) {
-                    if (c == 0) mbox[__popcll(vict & below)] = (ridx << 16) | (uint32_t)qs[(base & kQsMask) * 16];
-                    ++base;
-                }
-                wave_sync();
-                const uint32_t r = (uint32_t)__popcll(idle & below);
-                if (!active && r < pairs) {
-                    const uint32_t m = mbox[r];
-                    ridx = m >> 16;
-                    const f4 A = ray_o[ridx], D = ray_d[ridx];
-                    id = __float_as_uint(D.w);
-                    any = id >= 64u;
-                    o = xyz(A), d = xyz(D), tmax = A.w;
-                    bt = kINF, bk = -1;
-                    if (!any) {
-                        const unsigned long long key = best[id];
-                        if (key != ~0ull) bt = __uint_as_float((uint32_t)(key >> 32)), bk = (int)(uint32_t)key;
-                    }
-                    inv = rcp3(d);
-                    node = (int)(m & 0xffffu), sp = 0, base = 0;
-                    active = true;
-#if XRT_DEEP_EARLY
-                    have_next = false;
-#endif
-                }
-                wave_sync();   // the mailbox is rewritten next time
-            }
-        }
-#endif
         if (!__ballot(active)) break;
-#ifdef XRT_EXPERIMENTS
-        ++niter;
-        nsteps += (uint32_t)__popcll(__ballot(active) & kLeads);
-#endif
         if (!active) continue;
-#if XRT_DEEP_FLAT
         // ---- one node, with as few divergent branches as the step allows (the loop's exec-mask
         // bookkeeping cost about as many scalar instructions as it had vector ones): the node
         // from LDS or global memory through one generic pointer, every leaf triangle's test and
         // both reductions computed for closest-hit and any-hit rays alike, the stack top read
-        // every step.  Same decisions and results as the branchy form below.
+        // every step.  (Measured and not kept, DESIGN.md §3: a branchy form, fetching the likely
+        // next node before the leaf tests, work stealing between quads.)
         const f4* N = node < ntop ? top + 8 * node : P.bvh4 + 8 * (size_t)node;
         const f4 lo = N[c], hi = N[4 + c];
         const int cidx = __float_as_int(lo.w), ccnt = __float_as_int(hi.w);
@@ -592,145 +495,7 @@ __device__ __forceinline__ void wave_deep_walk(const KParams& P, const f4* top, 
             }
             active = false;
         }
-#else
-        // ---- one node: child c on lane c; lim = the quad's best t (closest hits) or tmax
-        f4 lo, hi;
-#if XRT_DEEP_EARLY
-        if (have_next) {
-            lo = nlo, hi = nhi;
-        } else
-#endif
-        if (node < ntop) {
-            lo = top[8 * node + c], hi = top[8 * node + 4 + c];
-        } else {
-            lo = ldg4(P.bvh4, 8 * (size_t)node + c), hi = ldg4(P.bvh4, 8 * (size_t)node + 4 + c);
-        }
-        const int cidx = __float_as_int(lo.w), ccnt = __float_as_int(hi.w);
-        float lim = any ? tmax : __uint_as_float(group_min32<4>(__float_as_uint(bt)));   // t >= 0: bits order
-#if XRT_DEEP_STEAL
-        if (!any) {   // other quads' finished subtrees of the same ray
-            const unsigned long long gk = best[id];
-            if (gk != ~0ull) lim = __builtin_fminf(lim, __uint_as_float((uint32_t)(gk >> 32)));
-        }
-#endif
-        const float e = ccnt >= 0 ? bvh_enter(lo, hi, o, inv, lim) : __builtin_inff();
-        bool done = false;
-#if XRT_DEEP_EARLY
-        // The likely next node — the nearest interior child overlapping [0, lim] before the leaf
-        // tests, else the stack top — is fetched now, so its latency overlaps the leaf loads.
-        // The leaf tests can only shrink lim: if that child still overlaps it is still the
-        // nearest and is taken; if not, no child does and the stack top is taken (unchanged).
-        int tnode = -1;
-        {
-            const bool inner0 = ccnt == 0 && e <= lim;
-            const uint32_t k0 = inner0 ? ((__float_as_uint(e) & ~3u) | (uint32_t)c) : ~0u;
-            const uint32_t m0 = group_min32<4>(k0);
-            if (m0 != ~0u) tnode = (int)group_or32<4>(k0 == m0 ? (uint32_t)cidx : 0u);
-            else if (sp > base) tnode = (int)qs[((sp - 1) & kQsMask) * 16];
-            if (tnode >= ntop) nlo = ldg4(P.bvh4, 8 * (size_t)tnode + c), nhi = ldg4(P.bvh4, 8 * (size_t)tnode + 4 + c);
-            else if (tnode >= 0) nlo = top[8 * tnode + c], nhi = top[8 * tnode + 4 + c];
-        }
-#endif
-#if XRT_DEEP_SPREAD
-        // The overlapped leaf children's triangles, dealt round robin over the quad's lanes
-        // (triangle j of the concatenated leaves to lane j % 4), so one leaf does not make one
-        // lane test its triangles serially while the other three wait.
-        bool oc = false;
-        {
-            const uint32_t mine = (ccnt > 0 && e != __builtin_inff()) ? (uint32_t)ccnt : 0u;
-            const uint32_t n0 = dpp32<0x00>(mine), n1 = dpp32<0x55>(mine), n2 = dpp32<0xAA>(mine), n3 = dpp32<0xFF>(mine);
-            const uint32_t f0 = dpp32<0x00>((uint32_t)cidx), f1 = dpp32<0x55>((uint32_t)cidx);
-            const uint32_t f2 = dpp32<0xAA>((uint32_t)cidx), f3 = dpp32<0xFF>((uint32_t)cidx);
-            const uint32_t p1 = n0, p2 = n0 + n1, p3 = p2 + n2, tot = p3 + n3;
-            constexpr int B = XRT_DEEP_LEAF_BATCH;
-            for (uint32_t j0 = (uint32_t)c; j0 < tot; j0 += 4u * B) {
-                f4 T[B][3];
-                bool ok[B];
-#pragma unroll
-                for (int b = 0; b < B; ++b) {
-                    const uint32_t j = j0 + 4u * (uint32_t)b;
-                    ok[b] = j < tot;
-                    if (ok[b]) {
-                        const uint32_t t = j < p1 ? f0 + j : j < p2 ? f1 + (j - p1) : j < p3 ? f2 + (j - p2) : f3 + (j - p3);
-                        const size_t i = 3 * (size_t)t;
-                        T[b][0] = ldg4(P.bvh_tri, i), T[b][1] = ldg4(P.bvh_tri, i + 1), T[b][2] = ldg4(P.bvh_tri, i + 2);
-                    }
-                }
-#pragma unroll
-                for (int b = 0; b < B; ++b) {
-                    if (!ok[b]) continue;
-                    if (any && T[b][1].w == 0.0f) continue;   // area-light objects never occlude
-                    float t;
-                    if (!ray_tri_nb(o, d, xyz(T[b][0]), xyz(T[b][1]), xyz(T[b][2]), t)) continue;
-                    if (any) {
-                        oc |= t < tmax;
-                    } else {
-                        const int k = __float_as_int(T[b][2].w);
-                        if (t < bt || (t == bt && k < bk)) bt = t, bk = k;
-                    }
-                }
-            }
-        }
-        if (any) {
-            done = group_or32<4>(oc ? 1u : 0u) != 0u;
-            if (done && c == 0) atomicOr(&occ[id & 63u], 1u << ((id >> 6) - 1u));
-        } else {
-            lim = __uint_as_float(group_min32<4>(__float_as_uint(__builtin_fminf(lim, bt))));
-        }
-#else
-        if (any) {
-            bool oc = false;
-            if (ccnt > 0 && e != __builtin_inff()) oc = deep_leaf<true>(P, cidx, ccnt, o, d, tmax, bt, bk);
-            done = group_or32<4>(oc ? 1u : 0u) != 0u;
-            if (done && c == 0) atomicOr(&occ[id & 63u], 1u << ((id >> 6) - 1u));
-        } else {
-            if (ccnt > 0 && e != __builtin_inff()) {
-                (void)deep_leaf<false>(P, cidx, ccnt, o, d, kINF, bt, bk);
-                lim = __builtin_fminf(lim, bt);   // this lane's leaf may have closed in
-            }
-            lim = __uint_as_float(group_min32<4>(__float_as_uint(lim)));
-        }
-#endif
-        if (!done) {
-            const bool inner = ccnt == 0 && e <= lim;   // interior child still overlapping [0, lim]
-            const uint32_t nkey = inner ? ((__float_as_uint(e) & ~3u) | (uint32_t)c) : ~0u;
-            const uint32_t nmin = group_min32<4>(nkey);
-            if (nmin != ~0u) {
-                const bool nearest = nkey == nmin;
-                const uint32_t m4 = (uint32_t)(__ballot(inner && !nearest) >> (lane & ~3)) & 0xfu;
-                if (inner && !nearest) qs[((sp + __popc(m4 & ((1u << c) - 1u))) & kQsMask) * 16] = (SE)cidx;
-                sp += __popc(m4);
-                node = (int)group_or32<4>(nearest ? (uint32_t)cidx : 0u);
-            } else if (sp == base) {
-                done = true;
-            } else {
-                node = (int)qs[((--sp) & kQsMask) * 16];
-            }
-        }
-#if XRT_DEEP_EARLY
-        have_next = !done && node == tnode;
-#endif
-        if (done) {
-            if (!any) {   // the quad's closest hit: the smallest (t bits, index) of the lanes
-                const uint64_t key = bk >= 0 ? ((uint64_t)__float_as_uint(bt) << 32) | (uint32_t)bk : ~0ull;
-                const uint64_t kmin = group_min64<4>(key);
-#if XRT_DEEP_STEAL
-                if (c == 0 && kmin != ~0ull) atomicMin(&best[id], kmin);
-#else
-                if (c == 0 && kmin != ~0ull) best[id] = kmin;
-#endif
-            }
-            active = false;
-        }
-#endif
     }
-#ifdef XRT_EXPERIMENTS
-    if (lane == 0) {
-        atomicAdd(P.stats + 38, (unsigned long long)n_deep), atomicAdd(P.stats + 39, (unsigned long long)nsteps);
-        atomicAdd(P.stats + 37, (unsigned long long)niter), atomicMax(P.stats + 36, (unsigned long long)niter);
-        atomicAdd(P.stats + 35, 1ull);
-    }
-#endif
 }
 
 // After merged_trace<NL, true> over the small objects: rank the rays whose segment still
@@ -769,53 +534,13 @@ __device__ __forceinline__ void deep_pass(const KParams& P, const f4* top, int n
     occ = W.occ[lane];
 }
 
-// Parking.  A wave's deep rays per visit are few (about 6 of its ~90 rays at C4) and their
-// walks differ in length, so walking them every visit (deep_pass) makes the wave wait for the
-// longest of a handful of walks each time.  Instead a slot whose rays still reach the BVH
-// after the small objects is parked: its rays join the wave's pool (Q: the ray records, the
-// slot's small-object closest-hit key and occlusion bits), it skips the visits that follow
-// (its path state stays in registers, untouched), and when enough slots are parked the wave
-// walks the whole pool at once — 16 quads fetching rays dynamically, bound by the pool's
-// total work rather than by one walk — and the parked slots resume with the merged results.
-// The slot's draws and sums happen in the same order whatever visit it resumes in.
-// Returns whether this lane parked.  Must be called by every lane (pool_n is wave-uniform).
-template <int NL>
-__device__ __forceinline__ bool deep_park(MergedWave<NL>& Q, uint32_t& pool_n, int lane, const f4 (&root)[4], bool ext,
-                                          v3 o, v3 d, uint32_t shm, const v3 (&so)[NL + 1], const v3 (&sd)[NL + 1],
-                                          const float (&stm)[NL + 1], unsigned long long best, uint32_t occ) {
-    constexpr int R = 1 + NL;
-    bool need[R];
-    const float bt = best == ~0ull ? kINF : __uint_as_float((uint32_t)(best >> 32));
-    need[0] = ext && root_overlap(root[0], root[1], root[2], root[3], o, rcp3(d), bt);
-    bool park = need[0];
-#pragma unroll
-    for (int l = 0; l < NL; ++l) {
-        need[1 + l] = ((shm & ~occ) >> l & 1u) && root_overlap(root[0], root[1], root[2], root[3], so[l], rcp3(sd[l]), stm[l]);
-        park |= need[1 + l];
-    }
-    if (park) Q.best[lane] = best, Q.occ[lane] = occ;
-#pragma unroll
-    for (int q = 0; q < R; ++q) {
-        const uint64_t m = __ballot(need[q]);
-        if (need[q]) {
-            const uint32_t at = pool_n + lanemask_rank(m);
-            const v3 ro = q == 0 ? o : so[q - 1], rd = q == 0 ? d : sd[q - 1];
-            Q.ro[at] = make_float4(ro.x, ro.y, ro.z, q == 0 ? kINF : stm[q - 1]);
-            Q.rd[at] = make_float4(rd.x, rd.y, rd.z, __uint_as_float((uint32_t)(q * 64 + lane)));
-        }
-        pool_n += (uint32_t)__popcll(m);
-    }
-    return park;
-}
-
 // LDS of k_step_merged<..., BVH = true> (bytes; the f4 regions 16-aligned): the small
 // objects' triangles (KParams::stri), the object and light tables, the first ntop 4-wide
-// BVH nodes, one MergedWave of trace scratch per wave, one MergedWave of parked rays per
-// wave (deep_park), then 16 quad stacks of bvh4_stack 16-bit entries per wave
+// BVH nodes, one MergedWave of trace scratch per wave, then 16 quad stacks of bvh4_stack 16-bit entries per wave
 // (use_step_bvh: at most 65,536 nodes).
-constexpr uint32_t kStackWave = 16u * kQs * 2u + 64u;   // a wave's 16 quad stacks (16-bit) + the steal mailbox
+constexpr uint32_t kStackWave = 16u * kQs * 2u;   // a wave's 16 quad stacks (16-bit entries)
 struct BvhStepLayout {
-    uint32_t tri, obj, light, top, wave, pool, stack, total;
+    uint32_t tri, obj, light, top, wave, stack, total;
     int ntop;
 };
 __host__ __device__ inline BvhStepLayout bvh_step_layout(const KParams& P, uint32_t wave_bytes) {
@@ -825,14 +550,12 @@ __host__ __device__ inline BvhStepLayout bvh_step_layout(const KParams& P, uint3
     B.light = B.obj + (uint32_t)sizeof(DObj) * (uint32_t)P.n_objs;
     B.top = (B.light + (uint32_t)sizeof(DLight) * (uint32_t)P.n_lights + 15u) & ~15u;
     // as many of the top XRT_BVH_TOP nodes as the rest leaves room for within kStepLds
-    const uint32_t pool_bytes = XRT_PARK ? (kBlock / 64) * wave_bytes : 0u;
-    const uint32_t rest = B.top + (kBlock / 64) * wave_bytes + pool_bytes + (kBlock / 64) * kStackWave;
+    const uint32_t rest = B.top + (kBlock / 64) * wave_bytes + (kBlock / 64) * kStackWave;
     const int fit = rest < kStepLds ? (int)((kStepLds - rest) / 128u) : 0;
     B.ntop = P.bvh4_nodes < XRT_BVH_TOP ? P.bvh4_nodes : XRT_BVH_TOP;
     B.ntop = B.ntop < fit ? B.ntop : fit;
     B.wave = B.top + 128u * (uint32_t)B.ntop;
-    B.pool = B.wave + (kBlock / 64) * wave_bytes;
-    B.stack = B.pool + pool_bytes;
+    B.stack = B.wave + (kBlock / 64) * wave_bytes;
     B.total = B.stack + (kBlock / 64) * kStackWave;
     return B;
 }
@@ -923,13 +646,13 @@ hipError_t launch_trace_2a_coop(const KParams& P, const uint32_t* list, const ui
 }
 
 // --------------------------------------------------------------- RNG refills ----
-// k_refill_merged: the ring refill of every schedule.  Same twist as wave_twist (libstdc++
-// _M_gen_rand: x[g+k] = x[g+k-227] ^ mix(x[g+k-624], x[g+k-623]), chunks k = m, 227+m,
-// 454+m held in registers), arranged for bandwidth: the old block is staged through LDS
-// (below), the next request's slot, stream position and old block are fetched while the
-// current one twists, and the slot state is not touched — the merged kernel clears
-// ST_RNGREQ when it next loads the slot, which is always after this kernel (one refill
-// launch follows every step launch).
+// k_refill_merged: every slot's first twist (the seeding refill after k_seed; later twists
+// happen in-line at the end of the step launch a slot runs low in, wave_refill).  Same twist
+// as wave_twist (libstdc++ _M_gen_rand: x[g+k] = x[g+k-227] ^ mix(x[g+k-624], x[g+k-623]),
+// chunks k = m, 227+m, 454+m held in registers), arranged for bandwidth: the old block is
+// staged through LDS (below), the next request's slot, stream position and old block are
+// fetched while the current one twists, and the slot state is not touched — the merged
+// kernel clears ST_RNGREQ when it first loads the slot, which is always after this kernel.
 
 
 // SPW: path slots per wave (64, 32 or 16), G: lanes per slot (1, or 64 / SPW for the group
@@ -940,8 +663,8 @@ hipError_t launch_trace_2a_coop(const KParams& P, const uint32_t* list, const ui
 // way, with few slots per GPU (a pixel shard of a multi-GPU frame) this puts more, shorter
 // waves on every SIMD.
 // BVH: two-level scenes (use_step_bvh: C4) — the small objects' triangles in LDS and traced
-// by merged_trace with original-index keys, the rest by the wave's BVH walk over the parked
-// slots' rays (deep_park); the hit triangle's shading data from global memory.  Same path
+// by merged_trace with original-index keys, the rest by the wave's BVH walk (deep_pass);
+// the hit triangle's shading data from global memory.  Same path
 // code otherwise.
 
 template <int INTEG, int NL, int SPW, int G, bool LANE, bool BVH>
@@ -958,7 +681,6 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
     LScene L;
     const DObjPlane* lplane = nullptr;
     MergedWave<NL>* Wp;
-    MergedWave<NL>* Qp = nullptr;   // BVH: the parked rays (deep_park)
     const f4* top = nullptr;   // BVH: the first ntop 4-wide nodes
     uint16_t* stk = nullptr;   // BVH: this wave's quad stacks
     int ntop = 0;
@@ -971,7 +693,6 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
         top = reinterpret_cast<const f4*>(lb + Bl.top);
         ntop = Bl.ntop;
         Wp = reinterpret_cast<MergedWave<NL>*>(lb + Bl.wave);
-        Qp = reinterpret_cast<MergedWave<NL>*>(lb + Bl.pool);
         stk = reinterpret_cast<uint16_t*>(lb + Bl.stack + (tid >> 6) * kStackWave);
         lds_copy(const_cast<f4*>(L.tri), P.stri, 3 * P.n_stri, tid);
         lds_copy(const_cast<DObj*>(L.obj), P.objs, P.n_objs, tid);
@@ -1129,47 +850,21 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
             start_sample();
         }
         __builtin_amdgcn_s_waitcnt(0);   // prologue loads done: the loop waits only on its own prefetches
-        bool parked = false, p_ext = false, pf_pending = false;   // BVH: parked slot; its ext_now; words in pf[]
-        uint32_t pool_n = 0;                                      // BVH: rays in the pool (wave-uniform)
+        bool pf_pending = false;   // BVH: words in pf[]
         for (uint32_t vis = 0; vis < visits; ++vis) {
             const bool act = live && !(st & ST_DONE) && g - rng.c >= (uint32_t)NW;
-            if (!__ballot(act || shm || parked)) break;
-            bool ext_now = act && ext;
-            bool proceed = true;   // this lane's trace is complete: shade it this visit
+            if (!__ballot(act || shm)) break;
+            const bool ext_now = act && ext;
             unsigned long long best;
             uint32_t occ;
-            if constexpr (BVH && !XRT_PARK) {
+            if constexpr (BVH) {
                 merged_trace<NL, true>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
                 deep_pass<NL, uint16_t>(P, top, ntop, stk, W, lane, root, ext_now, o, d, shm, so, sd, stm, best, occ);
-            } else if constexpr (BVH) {
-                ext_now = ext_now && !parked;
-                merged_trace<NL, true>(SO, L, W, lane, ext_now, o, d, parked ? 0u : shm, so, sd, stm, best, occ);
-                // a parked lane traced nothing this visit and passes no rays
-                const bool now = deep_park<NL>(Qp[tid >> 6], pool_n, lane, root, ext_now, o, d, parked ? 0u : shm, so,
-                                               sd, stm, best, occ);
-                if (now) parked = true, p_ext = ext_now;
-                proceed = !parked;
-                const uint32_t n_parked = (uint32_t)__popcll(__ballot(parked));
-                if (n_parked && (n_parked * 8u >= (uint32_t)SPW * XRT_PARK_EIGHTHS || vis + 1 == visits ||
-                                 !__ballot(proceed && (act || shm)))) {
-                    MergedWave<NL>& Q = Qp[tid >> 6];
-                    wave_sync();
-                    wave_deep_walk<uint16_t>(P, top, ntop, stk, Q.ro, Q.rd, Q.best, Q.occ, lane, pool_n);
-                    wave_sync();
-                    pool_n = 0;
-                    if (parked) {
-                        best = Q.best[lane], occ = Q.occ[lane];
-                        ext_now = p_ext;
-                        parked = false, proceed = true;
-                    }
-                    wave_sync();   // the pool is refilled from the next visit on
-                }
             } else if constexpr (!LANE) {
                 merged_trace<NL>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
             } else {
                 group_trace<NL, G>(P.n_objs, L, lplane, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
             }
-            if (!proceed) continue;   // BVH: parked until the pool is walked
             resolve(occ);
             if (BVH ? pf_pending : vis > 0) rng.take();   // the words prefetched at the end of the previous segment
             if (ext_now) {

@@ -39,6 +39,9 @@
 #ifndef XRT_PIX_WAVES
 #define XRT_PIX_WAVES 4      // min waves per SIMD (<= 128 VGPRs)
 #endif
+#ifndef XRT_PIX_PACKET
+#define XRT_PIX_PACKET 1     // traces walk the scene once per wave (coherent rays), not once per lane
+#endif
 
 // ---- the fused two-level schedule (k_step_merged<..., BVH = true>: C4)
 #ifndef XRT_BVH_WAVES
@@ -61,21 +64,6 @@
 #endif
 #ifndef XRT_DEEP_SPREAD
 #define XRT_DEEP_SPREAD 1    // a node's overlapped leaf triangles dealt over the quad's lanes (C4 -12%)
-#endif
-#ifndef XRT_DEEP_FLAT
-#define XRT_DEEP_FLAT 1      // the walk step with few divergent branches (leaf spread built in; no early / steal)
-#endif
-#ifndef XRT_DEEP_EARLY
-#define XRT_DEEP_EARLY 0     // fetch the likely next node before the leaf tests
-#endif
-#ifndef XRT_DEEP_STEAL
-#define XRT_DEEP_STEAL 0     // idle quads take stacked subtrees of active rays once the wave's rays are all taken
-#endif
-#ifndef XRT_PARK
-#define XRT_PARK 0           // park slots with deep rays and walk the pool in batches (C4 +40..+100%: not kept)
-#endif
-#ifndef XRT_PARK_EIGHTHS
-#define XRT_PARK_EIGHTHS 3   // ... once this many eighths of the wave's slots are parked
 #endif
 
 // ---- wavefront schedule (k_shade / k_trace*, XRT_FLAG_WAVEFRONT)

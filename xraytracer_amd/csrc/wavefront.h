@@ -8,10 +8,11 @@
 //   slots  : one path slot per pixel of this shard; all per-slot state is SoA (float4 /
 //            uint32 arrays indexed by slot) so a wave's loads are coalesced.
 //   RNG    : per slot a 1248-word ring (two 624-word mt19937 blocks) + cursor/generated
-//            counters.  A k_shade visit that finds fewer than kRngMin words left has its
-//            wave twist the slot's next block at the end of the same launch (wave_refill);
-//            the fused schedules put the slot on a refill list that k_refill_merged twists,
-//            one whole wave per listed ring.
+//            counters.  k_seed writes each slot's seeded state and one k_refill launch
+//            twists its first block; after that every schedule twists a slot's next block
+//            in-line, at the end of the launch in which it runs low, one whole wave per
+//            ring (wave_refill: k_shade, k_step, k_step_tri, k_step_merged).  k_pixel keeps
+//            its pixel's stream in LDS and generates it as it goes (pixel.hip).
 #pragma once
 #include <stdint.h>
 
@@ -60,7 +61,7 @@ enum : uint32_t {
     ST_REGEN = 8u,    // slot must start its next sample
     ST_DONE = 16u,    // all samples of this pixel are done
     ST_MEDIUM = 32u,  // VPT delta-tracking loop suspended (resumes after an RNG refill)
-    ST_RNGREQ = 64u,  // slot is on the refill list (k_refill twists its ring and clears this)
+    ST_RNGREQ = 64u,  // slot's first twist is pending (k_seed sets it, the seeding k_refill clears it)
     ST_NEEWALK = 128u,// VPT-NEE: the light sample's ratio tracking is suspended (state in KParams::nee)
     ST_SHADOW_SHIFT = 8u  // bits 8..15: which lights have a shadow ray in flight
 };

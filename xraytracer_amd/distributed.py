@@ -78,12 +78,15 @@ class ShardedRenderer:
     keep their old contents and the SUM reduce would add them once per rank, so render()
     raises ValueError for it."""
 
-    def __init__(self, renderer, dist=None, dst: int = 0):
+    def __init__(self, renderer, dist=None, dst: int = 0, time_reduce: bool = False):
         self.renderer = renderer
         self.dist = dist
         self.dst = dst
         self.rank, self.world = _world(dist)
-        self.last_reduce_s = 0.0   # host time of the last render()'s framebuffer reduce
+        # time_reduce: wait for each framebuffer reduce to complete and record its host time
+        # (bench.py); off by default, so callers can overlap the reduce with later work
+        self.time_reduce = time_reduce
+        self.last_reduce_s = 0.0   # host time of the last render()'s framebuffer reduce (time_reduce)
         if not 0 <= dst < self.world:
             raise ValueError(f"dst rank {dst} outside world of {self.world}")
 
@@ -101,12 +104,13 @@ class ShardedRenderer:
             after_stream = torch.cuda.current_stream(fb.device).cuda_stream
         st = self.renderer.render_device(scene, width, height, fb.data_ptr(), shard_index=self.rank,
                                          shard_count=self.world, after_stream=after_stream, **kw)
-        # the render has returned with the image complete; the reduce is timed on its own
-        # (host clock to its completion: the next render would wait for it anyway)
+        # the render has returned with the image complete; with time_reduce the reduce is
+        # timed on its own (host clock to its completion: the next render would wait for it)
         import time
         t0 = time.perf_counter()
         reduce_framebuffer(fb, self.dist, self.dst)
-        if self.world > 1 and fb.is_cuda:
-            torch.cuda.synchronize(fb.device)
-        self.last_reduce_s = time.perf_counter() - t0
+        if self.time_reduce:
+            if self.world > 1 and fb.is_cuda:
+                torch.cuda.synchronize(fb.device)
+            self.last_reduce_s = time.perf_counter() - t0
         return st
