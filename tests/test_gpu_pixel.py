@@ -94,6 +94,18 @@ def test_c3_family_long_chains(renderer):
     assert g.rng_twists >= g.path_slots * 2
 
 
+@pytest.mark.parametrize("wh", [(4, 3), (9, 5), (23, 13)])
+def test_frustum_lists_and_their_overflow(renderer, wh):
+    """Sphere-BVH scenes trace a pixel's camera rays against the spheres its widened jitter
+    pyramid meets (pix_frustum).  At 4x3 a pixel's pyramid holds far more than the list's 64
+    entries, so those pixels walk the BVH instead; 9x5 and 23x13 mix both kinds of pixels."""
+    w, h = wh
+    s = scenes.spheres(w, h)
+    img, ref, st, g = render_pixel(renderer, s, w, h, 150)
+    compare(img, ref)
+    counters_equal(g, st)
+
+
 @pytest.mark.parametrize("spp", [1, 2, 21, 31, 32, 33, 63, 64, 65, 127, 129, 300])
 def test_window_edges_two_lights(renderer, spp):
     """Two area lights (NL = 2: a surface hit draws 4 light words, so a chain skips 2

@@ -48,12 +48,14 @@ __device__ __forceinline__ bool sphere_bvh(const LScene& L, v3 o, v3 d, float tm
                 if (ANY && !(kw & (1 << 30))) continue;
                 const f4 S = L.ssph[j];
                 float t;
-                if (!sphere_hit(o, d, xyz(S), S.w, t)) continue;
+                const bool hit = sphere_hit(o, d, xyz(S), S.w, t);
                 if (ANY) {
-                    if (t < tmax) return true;
+                    if (hit && t < tmax) return true;
                 } else {
                     const int k = kw & 0x3fffffff;
-                    if (t < bt || (t == bt && k < bk)) bt = t, bk = k;
+                    const bool upd = hit && (t < bt || (t == bt && k < bk));
+                    bt = upd ? t : bt;
+                    bk = upd ? k : bk;
                 }
             }
         }
@@ -238,14 +240,15 @@ __device__ __forceinline__ bool sphere_bvh_wave(const LScene& L, v3 o, v3 d, flo
                 const int kw = wave_uniform(L.sbk[j]);
                 if (ANY && !(kw & (1 << 30))) continue;
                 const f4 S = L.ssph[j];
-                float t;
-                if (ov && sphere_hit(o, d, xyz(S), S.w, t)) {
-                    if (ANY) {
-                        if (t < tmax) occ = true;
-                    } else {
-                        const int k = kw & 0x3fffffff;
-                        if (t < bt || (t == bt && k < bk)) bt = t, bk = k;
-                    }
+                float t = 0.0f;
+                const bool hit = ov && sphere_hit(o, d, xyz(S), S.w, t);
+                if (ANY) {
+                    occ = occ || (hit && t < tmax);
+                } else {
+                    const int k = kw & 0x3fffffff;
+                    const bool upd = hit && (t < bt || (t == bt && k < bk));
+                    bt = upd ? t : bt;
+                    bk = upd ? k : bk;
                 }
             }
             if (ANY && __ballot(active && !occ) == 0ull) return occ;

@@ -333,7 +333,16 @@ __device__ __forceinline__ bool ray_tri(v3 o, v3 d, v3 v0, v3 e1, v3 e2, float& 
     return t > kEPSILON;
 }
 
-// Sphere::doIntersect + solveQuadratic (Src/primitive.h:133-177): double -0.5*(b±sqrt)
+// Sphere::doIntersect + solveQuadratic (Src/primitive.h:133-177): double -0.5*(b±sqrt).
+// Past the discriminant test (a wave whose rays all miss skips the rest) the lanes compute
+// the general root pair and select, so rays with different outcomes run one instruction
+// stream (the branchy form spent about as many scalar exec-mask instructions as vector ones).
+// Same values as the reference's branches:
+//  * discr < 0: no hit (a NaN discriminant passes on, as in the reference, and yields NaN
+//    roots, which every caller's `t < best` rejects);
+//  * discr == 0: t0 = t1 = -0.5 * b / a in double — rare, so it keeps its own branch;
+//  * q = -0.5 * (b ± sqrt): b - sq is b + (-sq) exactly;
+//  * the swap and the t0 < 0 fallback as selects.
 __device__ __forceinline__ bool sphere_hit(v3 o, v3 d, v3 c, float r, float& tnear) {
     const v3 L = o - c;
     const float a = dot(d, d);
@@ -341,22 +350,15 @@ __device__ __forceinline__ bool sphere_hit(v3 o, v3 d, v3 c, float r, float& tne
     const float cc = dot(L, L) - r * r;
     const float discr = b * b - 4.0f * a * cc;
     if (discr < 0.0f) return false;
-    float t0, t1;
-    if (discr == 0.0f) {
-        t0 = t1 = (float)(-0.5 * (double)b / (double)a);
-    } else {
-        const double sq = __builtin_sqrt((double)discr);
-        const float q = (b > 0.0f) ? (float)(-0.5 * ((double)b + sq)) : (float)(-0.5 * ((double)b - sq));
-        t0 = q / a;
-        t1 = cc / q;
-    }
-    if (t0 > t1) { const float tmp = t0; t0 = t1; t1 = tmp; }
-    if (t0 < 0.0f) {
-        t0 = t1;
-        if (t0 < 0.0f) return false;
-    }
-    tnear = t0;
-    return true;
+    const double sq = __builtin_sqrt((double)discr);
+    const float q = (float)(-0.5 * ((double)b + (b > 0.0f ? sq : -sq)));
+    float t0 = q / a;
+    float t1 = cc / q;
+    if (discr == 0.0f) t0 = t1 = (float)(-0.5 * (double)b / (double)a);
+    const bool sw = t0 > t1;
+    const float lo = sw ? t1 : t0, hi = sw ? t0 : t1;
+    tnear = lo < 0.0f ? hi : lo;
+    return !(lo < 0.0f && hi < 0.0f);
 }
 
 // BoxMesh::intersect slab test (Src/primitive.h:243-264)

@@ -45,7 +45,9 @@ namespace xrt {
 
 constexpr int kPixBlock = XRT_PIX_BLOCK;           // threads per block: 8 waves share one LDS scene copy
 constexpr uint32_t kPixSumStride = 68;             // ordered-sum buffer row (floats): 64 + 4, rows on other banks
-constexpr uint32_t kPixWaveLds = (kMT + 3 * kPixSumStride) * 4;   // per wave: stream window + sum buffer
+constexpr uint32_t kPixList = 64;                   // camera-frustum sphere list entries per wave (16-bit)
+constexpr uint32_t kPixWaveLds = (kMT + 3 * kPixSumStride) * 4 + kPixList * 2;   // stream + sum buffer + list
+constexpr uint32_t kPixFrustumMax = XRT_PIX_FRUSTUM_MAX;   // sphere scenes up to this size build the lists
 
 constexpr bool kPixPacket = XRT_PIX_PACKET != 0;   // wave-uniform scene walks (lscene.h closest_w)
 
@@ -84,6 +86,78 @@ __device__ __forceinline__ void pix_gen(uint32_t* st, uint32_t g, int lane) {
     wave_sync();
 }
 
+// The spheres a camera ray of pixel (col, row) can hit, for sphere-BVH scenes (C3): every
+// camera ray of a pixel leaves the camera origin o through its jitter square, so it lies in
+// the pyramid spanned by the square's corner directions — widened here by 0.01 pixel on every
+// side, far beyond the float error of div_w / div_h / camera_ray's direction (~1e-7 relative
+// against 1e-5 of the pixel's angle).  A ray that Sphere::intersect reports hitting passes
+// within float error of the sphere, i.e. through the ball of radius |r| + sph_pad around it
+// (sph_pad, the BVH's own box margin, is orders of magnitude above that error), and a ball
+// that meets the pyramid is on the inner side of (or crosses) all four side planes.  So the
+// list holds every sphere any of the pixel's camera rays can hit (and a few more), and its
+// windows test only those, in any order: the closest hit is the (t, index) minimum either way.
+// Each lane tests 1/64 of the spheres; returns the list length, or -1 when it overflows
+// kPixList (the pixel's camera rays then walk the BVH).  Every lane must call it.
+template <int SCN>
+__device__ int pix_frustum(const KParams& P, const LScene& L, uint32_t col, uint32_t row, uint16_t* list, int lane) {
+    const float m = 0.01f;
+    const float u0 = ((float)col - m) / P.fw, u1 = ((float)col + (1.0f + m)) / P.fw;
+    const float v0 = ((float)row - m) / P.fh, v1 = ((float)row + (1.0f + m)) / P.fh;
+    const float* x = P.c2w;
+    auto world = [&](float u, float v) {
+        const v3 dir = mk((2.0f * u - 1.0f) * P.scale, (1.0f - 2.0f * v) * P.scale / P.aspect, -1.0f);
+        return mk(dir.x * x[0] + dir.y * x[4] + dir.z * x[8], dir.x * x[1] + dir.y * x[5] + dir.z * x[9],
+                  dir.x * x[2] + dir.y * x[6] + dir.z * x[10]);
+    };
+    const v3 D0 = world(u0, v0), D1 = world(u1, v0), D2 = world(u1, v1), D3 = world(u0, v1);
+    const v3 Dc = (D0 + D1) + (D2 + D3);
+    v3 n[4] = {cross(D0, D1), cross(D1, D2), cross(D2, D3), cross(D3, D0)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float s = dot(n[k], Dc) < 0.0f ? -1.0f : 1.0f;
+        n[k] = n[k] * (s / length(n[k]));   // unit normal pointing into the pyramid
+    }
+    const v3 o = mk(x[12], x[13], x[14]);
+    uint32_t cnt = 0;
+    for (int base = 0; base < P.n_sph; base += 64) {
+        const int j = base + lane;
+        bool in = false;
+        if (j < P.n_sph) {
+            const f4 S = L.ssph[j];
+            const v3 c = xyz(S) - o;
+            const float rr = -(__builtin_fabsf(S.w) + P.sph_pad);
+            in = dot(n[0], c) >= rr && dot(n[1], c) >= rr && dot(n[2], c) >= rr && dot(n[3], c) >= rr;
+        }
+        const uint64_t mk_ = __ballot(in);
+        const uint32_t at = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk_ >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk_, 0u));
+        if (in && at < kPixList) list[at] = (uint16_t)j;
+        cnt += (uint32_t)__builtin_popcountll(mk_);
+    }
+    wave_sync();
+    return cnt <= kPixList ? (int)cnt : -1;
+}
+
+// Scene::intersect over a pixel's frustum list (pix_frustum): the (t, index) minimum over the
+// listed spheres, as sphere_bvh's
+__device__ __forceinline__ void closest_list(const LScene& L, const uint16_t* list, int nlist, v3 o, v3 d, HitRec& h,
+                                             bool active) {
+    h.t = kINF, h.u = h.v = 0.0f, h.code = -1, h.surf = -1, h.dp = -1, h.t1 = kINF;
+    h.st = h.su = h.sv = h.du = h.dv = 0.0f;
+    float bt = kINF;
+    int bk = -1;
+    for (int e = 0; e < nlist; ++e) {
+        const int j = wave_uniform((int)list[e]);
+        const f4 S = L.ssph[j];
+        const int k = wave_uniform(L.sbk[j]) & 0x3fffffff;
+        float t = 0.0f;
+        const bool hit = active && sphere_hit(o, d, xyz(S), S.w, t);
+        const bool upd = hit && (t < bt || (t == bt && k < bk));
+        bt = upd ? t : bt;
+        bk = upd ? k : bk;
+    }
+    if (bk >= 0) h.t = bt, h.code = (1 << 28) | bk;
+}
+
 // LDS bytes of the pixel schedule: the scene carve, then kPixWaveLds per wave
 __host__ __device__ inline uint32_t pix_wave_off(const KParams& P) { return (step_layout(P).total + 15u) & ~15u; }
 
@@ -95,7 +169,9 @@ __global__ __launch_bounds__(kPixBlock, XRT_PIX_WAVES) void k_pixel(KParams P, u
     const LScene L = load_lscene(P, lb, tid, kPixBlock);
     uint32_t* st = reinterpret_cast<uint32_t*>(lb + pix_wave_off(P) + (tid >> 6) * kPixWaveLds);
     float* sum = reinterpret_cast<float*>(st + kMT);
+    uint16_t* list = reinterpret_cast<uint16_t*>(sum + 3 * kPixSumStride);
     __syncthreads();
+    const bool frustum = SCN == SCN_SPHERE && L.n_snode > 0 && P.n_sph <= (int)kPixFrustumMax;
     // words a surface hit draws beyond its jitter, in pairs: one pair per area light (Direct)
     const uint32_t NLD = INTEG == XRT_INTEGRATOR_DIRECT ? (uint32_t)P.n_lights : 0u;
     for (;;) {
@@ -116,6 +192,7 @@ __global__ __launch_bounds__(kPixBlock, XRT_PIX_WAVES) void k_pixel(KParams P, u
                 if ((uint32_t)lane + 64u * k < kMT / 4) reinterpret_cast<u32x4*>(st)[lane + 64 * k] = v[k];
             wave_sync();
         }
+        const int nlist = frustum ? pix_frustum<SCN>(P, L, col, row, list, lane) : -1;
         float* px = P.fb + 3 * ((size_t)col + (size_t)P.width * row);
         float acc = lane < 3 ? px[lane] : 0.0f;   // lane c < 3: channel c of the running sum
         uint32_t o = kMT, g = kMT, k = 0;        // next draw x[o]; x[0 .. g) generated
@@ -145,7 +222,12 @@ __global__ __launch_bounds__(kPixBlock, XRT_PIX_WAVES) void k_pixel(KParams P, u
             }
             {
                 HitRec h;
-                if (kPixPacket) closest_w<SCN>(P, L, ro, rd, h, cand);
+#ifdef XRT_PIX_EXP_NOTRACE
+                h.code = (cand && (rng.i & 6u) == 2u) ? (1 << 28) : -1; h.t = 5.0f; h.u = h.v = 0.0f; h.surf = h.dp = -1;
+                if (false)
+#endif
+                if (nlist >= 0) closest_list(L, list, nlist, ro, rd, h, cand);
+                else if (kPixPacket) closest_w<SCN>(P, L, ro, rd, h, cand);
                 else if (cand) closest_l<SCN>(P, L, ro, rd, h);
                 if (cand) {
                     obj = surface_l<SCN>(L, ro, rd, h, S);
@@ -157,25 +239,45 @@ __global__ __launch_bounds__(kPixBlock, XRT_PIX_WAVES) void k_pixel(KParams P, u
             const uint64_t smask = NLD ? (uint64_t)__ballot(kind == 2) : 0ull;
             uint64_t M = 0;
             uint32_t cnt = 0, pos = 0;
-            while (pos < 64u && cnt < rem) {
-                const uint64_t ahead = smask >> pos;
-                const uint32_t q = ahead ? pos + (uint32_t)__builtin_ctzll(ahead) : 64u;
-                uint32_t run = q - pos;   // samples without a surface hit, then the one at q
-                if (run > rem - cnt) run = rem - cnt;
-                M |= (run == 64u ? ~0ull : ((1ull << run) - 1ull)) << pos;
-                cnt += run;
-                pos += run;
-                if (cnt == rem || q == 64u) break;   // sample budget reached, or the window ends
-                M |= 1ull << q;   // pos == q here
-                ++cnt;
-                pos = q + 1u + NLD;
+            if (NLD == 1 && rem >= 64u) {
+                // one light, a full window (bit-parallel): a surface-hit sample skips the next
+                // candidate, so within a run of surface hits that starts on the chain every
+                // other candidate is a sample.  kill = the surface hits on the chain: a run's
+                // even offsets from its start (the carry of s + start clears exactly the runs
+                // that start at even positions), M = every candidate not right after a kill.
+                constexpr uint64_t kEven = 0x5555555555555555ull;
+                const uint64_t start = smask & ~(smask << 1);
+                const uint64_t even_runs = smask & ~(smask + (start & kEven));
+                const uint64_t kill = (even_runs & kEven) | (smask & ~even_runs & ~kEven);
+                M = ~(kill << 1);
+                cnt = (uint32_t)__builtin_popcountll(M);
+                const uint32_t last = 63u - (uint32_t)__builtin_clzll(M);
+                pos = last + 1u + (uint32_t)((kill >> last) & 1ull);
+            } else {
+                while (pos < 64u && cnt < rem) {
+                    const uint64_t ahead = smask >> pos;
+                    const uint32_t q = ahead ? pos + (uint32_t)__builtin_ctzll(ahead) : 64u;
+                    uint32_t run = q - pos;   // samples without a surface hit, then the one at q
+                    if (run > rem - cnt) run = rem - cnt;
+                    M |= (run == 64u ? ~0ull : ((1ull << run) - 1ull)) << pos;
+                    cnt += run;
+                    pos += run;
+                    if (cnt == rem || q == 64u) break;   // sample budget reached, or the window ends
+                    M |= 1ull << q;   // pos == q here
+                    ++cnt;
+                    pos = q + 1u + NLD;
+                }
             }
             const bool member = (M >> lane) & 1ull;
             v3 rad = mk(0, 0, 0);
             if (INTEG == XRT_INTEGRATOR_DIRECT) {
                 // DirectIntegrator::integrate (Src/integrator.h:82-119); the light loop runs on
                 // every lane (the shadow trace is a wave walk), shading where a sample hit a surface
+#ifdef XRT_PIX_EXP_NOSHADE
+                const bool shade = false;
+#else
                 const bool shade = member && kind == 2;
+#endif
                 if (member && kind == 0) rad = mk((float)0.18, (float)0.18, (float)0.18);
                 if (member && kind == 1) rad = light_Le(L.light[L.obj[obj].light], S.ns, rd);
                 for (int l = 0; l < P.n_lights; ++l) {
@@ -210,7 +312,11 @@ __global__ __launch_bounds__(kPixBlock, XRT_PIX_WAVES) void k_pixel(KParams P, u
                 sum[rank] = r.x, sum[kPixSumStride + rank] = r.y, sum[2 * kPixSumStride + rank] = r.z;
             }
             wave_sync();
+#ifdef XRT_PIX_EXP_NOSUM
+            if (false) {
+#else
             if (lane < 3) {
+#endif
                 const f4* q4 = reinterpret_cast<const f4*>(sum + kPixSumStride * lane);
                 const uint32_t nv = (uint32_t)__builtin_popcountll(vm);
                 for (uint32_t j = 0; j < nv; j += 8) {

@@ -205,6 +205,7 @@ struct KParams {
     const f4* ssph;           // spheres in BVH leaf order (center, radius)
     const int* sbk;           // per ssph entry: original sphere index | (occluder << 30)
     int n_snode;
+    float sph_pad;            // the sphere BVH's box margin (1e-4 scene diagonal + 1e-4)
     int n_segs, n_lights, n_tris, n_sph, n_box, scene_kind, n_objs, small_tri;
     int det_bounded;   // every triangle has |e1| |e2| < 2^120 (ray_tri_nb's Newton reciprocal, xrt_api.cpp)
     DMedium medium;

@@ -550,7 +550,7 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
     // Sphere boxes: center +- radius, padded by 1e-4 of the scene diagonal + 1e-4 —
     // far above the float error of Sphere::intersect's hit point (and of its
     // near-tangent discriminant), so a box test never drops a hit the linear scan accepts.
-    P.snode = nullptr, P.ssph = nullptr, P.sbk = nullptr, P.n_snode = 0;
+    P.snode = nullptr, P.ssph = nullptr, P.sbk = nullptr, P.n_snode = 0, P.sph_pad = 0.0f;
     if (P.scene_kind == SCN_SPHERE && P.n_sph >= kSphBvhMin && !exp_env("XRT_NO_BVH")) {
         const size_t ns = (size_t)P.n_sph;
         std::vector<float> mn(3 * ns), mx(3 * ns);
@@ -564,7 +564,8 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
         }
         const float diag = std::sqrt((hi[0] - lo[0]) * (hi[0] - lo[0]) + (hi[1] - lo[1]) * (hi[1] - lo[1]) +
                                      (hi[2] - lo[2]) * (hi[2] - lo[2]));
-        const BvhBuild B = build_bvh(mn.data(), mx.data(), (uint32_t)ns, kBvhLeaf, 1e-4f * diag + 1e-4f, kBvhMaxDepth);
+        P.sph_pad = 1e-4f * diag + 1e-4f;
+        const BvhBuild B = build_bvh(mn.data(), mx.data(), (uint32_t)ns, kBvhLeaf, P.sph_pad, kBvhMaxDepth);
         const std::vector<SkipNode> T = thread_bvh(B);
         std::vector<f4> bs(ns);
         std::vector<int> bk(ns);
