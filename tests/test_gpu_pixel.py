@@ -160,6 +160,27 @@ def test_accumulate_and_rejects(renderer):
     assert st["rejected"] > 1000
 
 
+def test_deferred_shading_rejects_and_accumulate(renderer):
+    """Direct on a sphere scene queues its surface hits and shades three windows at once
+    (pixel.hip deferred shading); the pending samples keep their order through the flush:
+    a sphere light with negative green radiance makes every sample that sees it (directly or
+    through a light sample) rejected, samples are added to a nonzero image, and spp values
+    end the chain at every point of a flush cycle."""
+    s = scenes.SceneBundle()
+    for k in range(30):
+        x, z = -3.0 + (k % 6) * 1.2, -2.0 - (k // 6) * 1.2
+        s.add_sphere(f"s{k:02d}", (x, 0.0, z), 0.5, (0.7, 0.5, 0.3))
+    s.add_sphere_light("SphereLight", (0.5, 2.5, -4.0), 1.0, (20.0, -1.0, 20.0))
+    s.flatten()
+    s.camera = scenes.pinhole((1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 3, 4, 1), 60.0, 32, 24)
+    init = np.random.default_rng(4).uniform(0.0, 2.0, (24, 32, 3)).astype(np.float32)
+    for spp in (5, 64, 130, 191, 257):
+        img, ref, st, g = render_pixel(renderer, s, 32, 24, spp, integrator="direct", initial=init)
+        compare(img, ref)
+        counters_equal(g, st)
+        assert st["rejected"] > 0
+
+
 def test_shards_and_step_schedule_agree(renderer):
     """Row shards of the pixel schedule reassemble the whole frame bit for bit, and the
     per-slot fused schedule (XRT_FLAG_NO_PIXEL) renders the same image."""

@@ -1,6 +1,6 @@
 set -u
-O=gpurun_out/r05g; mkdir -p $O
+O=gpurun_out/r05h; mkdir -p $O
 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_pixel.py -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; tail -2 $O/tests.log; if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" $O/tests.log | head -8; exit $rc; fi
-bash tools/ab.sh r05g -b "C3" -s "C3:8" -r 2 default nofrustum || exit $?
-for l in default nofrustum; do tools/pmc_quick.sh r05g C3 $l || exit $?; done
+bash tools/ab.sh r05h -b "C3" -s "C3:8" -r 2 default nodefer || exit $?
+for l in default nodefer; do tools/pmc_quick.sh r05h C3 $l || exit $?; done

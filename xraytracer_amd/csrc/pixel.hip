@@ -158,22 +158,51 @@ __device__ __forceinline__ void closest_list(const LScene& L, const uint16_t* li
     if (bk >= 0) h.t = bt, h.code = (1 << 28) | bk;
 }
 
-// LDS bytes of the pixel schedule: the scene carve, then kPixWaveLds per wave
+// Deferred shading (Direct on sphere-BVH scenes): a window's samples that hit a surface are
+// ~1/4 of its lanes, so shading them in the window (light samples, the shadow rays' wave walk)
+// would run the wave at a quarter of its width.  Instead they join a queue of up to 64 shading
+// items (the candidate's stream position and hit record), and every sample of the window
+// leaves a one-byte code in a pending list: 0 = the miss radiance 0.18, 1 + l = light l's Le
+// (an area light seen from its front), 255 = zero (seen from the back), 128 + i = queue item
+// i.  Every third window (or when the queue might overflow, or the pixel is done) the queue is
+// shaded by the whole wave at once and the pending codes are added to the running sum in
+// sample order.  An item's words are still in the 624-word stream window then: three windows
+// span at most 3 * (128 + 2 NL) words and generation runs at most 255 + 2 NL past the current
+// window's start, within 624 for NL <= 18.  Same draws, same rays, same float sums.
+constexpr bool pix_defer(int scn, int integ) {
+    return XRT_PIX_DEFER && scn == SCN_SPHERE && integ == XRT_INTEGRATOR_DIRECT;
+}
+constexpr uint32_t kPixPend = 192;   // pending samples of three windows (codes)
+constexpr uint32_t kPixWaveDeferLds = kPixWaveLds + 3 * kPixSumStride * 4 + 3 * 64 * 4 + kPixPend;
+constexpr int pix_block(int scn, int integ) { return pix_defer(scn, integ) ? 1024 : kPixBlock; }
+__host__ __device__ inline bool pix_defer_rt(const KParams& P) {
+    return XRT_PIX_DEFER && P.scene_kind == SCN_SPHERE && P.integrator == XRT_INTEGRATOR_DIRECT;
+}
+
+// LDS bytes of the pixel schedule: the scene carve, then one slice per wave
 __host__ __device__ inline uint32_t pix_wave_off(const KParams& P) { return (step_layout(P).total + 15u) & ~15u; }
 
-template <int SCN, int INTEG>
-__global__ __launch_bounds__(kPixBlock, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t* __restrict__ work) {
+template <int SCN, int INTEG, int BS>
+__global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t* __restrict__ work) {
+    constexpr bool DEFER = pix_defer(SCN, INTEG);
+    constexpr uint32_t kWave = DEFER ? kPixWaveDeferLds : kPixWaveLds;
     extern __shared__ __attribute__((aligned(16))) f4 lds_pix[];
     char* lb = reinterpret_cast<char*>(lds_pix);
     const int tid = threadIdx.x, lane = tid & 63;
-    const LScene L = load_lscene(P, lb, tid, kPixBlock);
-    uint32_t* st = reinterpret_cast<uint32_t*>(lb + pix_wave_off(P) + (tid >> 6) * kPixWaveLds);
+    const LScene L = load_lscene(P, lb, tid, BS);
+    uint32_t* st = reinterpret_cast<uint32_t*>(lb + pix_wave_off(P) + (tid >> 6) * kWave);
     float* sum = reinterpret_cast<float*>(st + kMT);
     uint16_t* list = reinterpret_cast<uint16_t*>(sum + 3 * kPixSumStride);
+    float* ires = reinterpret_cast<float*>(list + kPixList);        // DEFER: shaded items' radiance
+    uint32_t* it_i = reinterpret_cast<uint32_t*>(ires + 3 * kPixSumStride);   // item: jitter word's slot
+    float* it_t = reinterpret_cast<float*>(it_i + 64);                        // item: hit t
+    int* it_c = reinterpret_cast<int*>(it_t + 64);                            // item: hit code
+    uint8_t* codes = reinterpret_cast<uint8_t*>(it_c + 64);                   // pending samples
     __syncthreads();
     const bool frustum = SCN == SCN_SPHERE && L.n_snode > 0 && P.n_sph <= (int)kPixFrustumMax;
     // words a surface hit draws beyond its jitter, in pairs: one pair per area light (Direct)
     const uint32_t NLD = INTEG == XRT_INTEGRATOR_DIRECT ? (uint32_t)P.n_lights : 0u;
+    const uint32_t per_window = (64u + NLD) / (1u + NLD);   // most surface hits one window's chain holds
     for (;;) {
         uint32_t s = 0;
         if (lane == 0) s = atomicAdd(work, 1u);
@@ -197,6 +226,101 @@ __global__ __launch_bounds__(kPixBlock, XRT_PIX_WAVES) void k_pixel(KParams P, u
         float acc = lane < 3 ? px[lane] : 0.0f;   // lane c < 3: channel c of the running sum
         uint32_t o = kMT, g = kMT, k = 0;        // next draw x[o]; x[0 .. g) generated
         uint32_t nsh = 0, nrej = 0;
+        uint32_t qn = 0, pn = 0, pw = 0;         // DEFER: queued items, pending samples, windows since a flush
+
+        // Image::addPixel in sample order for the lanes of vm (lane order), each with value r:
+        // ranked into the sum buffer, then added one after the other by lanes 0..2 (a channel each)
+        auto add_in_order = [&](uint64_t vm, v3 r) {
+            if ((vm >> lane) & 1ull) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(vm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)vm, 0u));
+                sum[rank] = r.x, sum[kPixSumStride + rank] = r.y, sum[2 * kPixSumStride + rank] = r.z;
+            }
+            wave_sync();
+            if (lane < 3) {
+                const float* q = sum + kPixSumStride * lane;
+                const f4* q4 = reinterpret_cast<const f4*>(q);
+                const uint32_t nv = (uint32_t)__builtin_popcountll(vm);
+                uint32_t j = 0;
+                for (; j + 8 <= nv; j += 8) {
+                    const f4 a = q4[j / 4], b = q4[j / 4 + 1];
+                    acc = acc + a.x, acc = acc + a.y, acc = acc + a.z, acc = acc + a.w;
+                    acc = acc + b.x, acc = acc + b.y, acc = acc + b.z, acc = acc + b.w;
+                }
+                for (; j < nv; ++j) acc = acc + q[j];
+            }
+            wave_sync();   // the buffer is rewritten next time
+        };
+        // integrate(...) / pdf (pinhole pdf 1) and the invalid-radiance check (Src/renderer.cpp:53-73)
+        auto invalid = [](v3 r) {
+            return __builtin_isnan(r.x) || __builtin_isnan(r.y) || __builtin_isnan(r.z) || __builtin_isinf(r.x) ||
+                   __builtin_isinf(r.y) || __builtin_isinf(r.z) || r.x < 0.0f || r.y < 0.0f || r.z < 0.0f;
+        };
+        // DirectIntegrator's light loop for a sample at surface S (Src/integrator.h:94-110), every
+        // lane (the shadow rays are a wave walk); `shade`: this lane's sample hit a surface
+        auto direct_light = [&](bool shade, const Surf& S, int obj, LdsRng& rng, v3& rad) {
+            for (int l = 0; l < P.n_lights; ++l) {
+                v3 wi = mk(0, 0, 0), Lv = mk(0, 0, 0);
+                float tmax = 0.0f, pdf = 0.0f;
+                if (shade) Lv = light_sample(L.light[l], S.pos, wi, pdf, tmax, rng);
+                const bool ray = shade && pdf != 0.0f;
+                const float bias = 0.01f;
+                nsh += ray ? 1u : 0u;
+                bool vis = true;
+                if (kPixPacket) vis = !occluded_w<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias, ray);
+                else if (ray) vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias);
+                if (ray) {
+                    const float cosv = smax(0.0f, dot(S.ng, wi));
+                    const v3 fr = eval_bxdf(L.obj[obj]);
+                    rad = rad + div3s(((fr * (float)vis) * Lv) * cosv, pdf);
+                }
+            }
+        };
+        // DEFER: shade the queue (lane i: item i), then add the pending samples in order
+        auto flush = [&]() {
+            const bool act = (uint32_t)lane < qn;
+            v3 rad = mk(0, 0, 0);
+            Surf S;
+            int obj = -1;
+            LdsRng rng{st, act ? it_i[lane] : 0u};
+            if (act) {
+                // the item's camera ray again (its jitter words), and its hit record
+                const float u = div_w(P, (float)(int)col + rng.next());
+                const float v = div_h(P, (float)(int)row + rng.next());
+                v3 ro, rd;
+                camera_ray(P, u, v, ro, rd);
+                HitRec h;
+                h.t = it_t[lane], h.u = h.v = 0.0f, h.code = it_c[lane], h.surf = -1, h.dp = -1, h.t1 = kINF;
+                h.st = h.su = h.sv = h.du = h.dv = 0.0f;
+                obj = surface_l<SCN>(L, ro, rd, h, S);
+            }
+            direct_light(act, S, obj, rng, rad);
+            const v3 r = rad / 1.0f;
+            const uint64_t badm = __ballot(act && invalid(r));
+            if (act) ires[lane] = r.x, ires[kPixSumStride + lane] = r.y, ires[2 * kPixSumStride + lane] = r.z;
+            wave_sync();
+            for (uint32_t base = 0; base < pn; base += 64) {
+                const uint32_t m = base + (uint32_t)lane;
+                const bool in = m < pn;
+                const uint32_t code = in ? codes[m] : 0u;
+                v3 val = mk((float)0.18, (float)0.18, (float)0.18);   // miss: Vec3f(0.18) / 1
+                bool ok = true;
+                if (code == 255u) {
+                    val = mk(0, 0, 0) / 1.0f;
+                } else if (code >= 128u) {
+                    const uint32_t i = code - 128u;
+                    val = mk(ires[i], ires[kPixSumStride + i], ires[2 * kPixSumStride + i]);
+                    ok = !((badm >> i) & 1ull);
+                } else if (code > 0u) {
+                    val = ld3(L.light[code - 1u].Le) / 1.0f;
+                    ok = !invalid(val);
+                }
+                const uint64_t vm = __ballot(in && ok);
+                nrej += (uint32_t)(__builtin_popcountll(__ballot(in)) - __builtin_popcountll(vm));
+                add_in_order(vm, val);
+            }
+            qn = 0, pn = 0, pw = 0;
+        };
+
         while (k < P.spp) {
             const uint32_t rem = P.spp - k;
             // candidates that can lie on the chain: rem samples advance at most 1 + NLD each
@@ -214,25 +338,19 @@ __global__ __launch_bounds__(kPixBlock, XRT_PIX_WAVES) void k_pixel(KParams P, u
             LdsRng rng{st, ci};
             v3 ro = mk(0, 0, 0), rd = mk(0, 0, 0);
             Surf S;
+            HitRec h;
             int obj = -1, kind = 0;   // 0 miss, 1 area light, 2 surface
             if (cand) {
                 const float u = div_w(P, (float)(int)col + rng.next());
                 const float v = div_h(P, (float)(int)row + rng.next());
                 camera_ray(P, u, v, ro, rd);
             }
-            {
-                HitRec h;
-#ifdef XRT_PIX_EXP_NOTRACE
-                h.code = (cand && (rng.i & 6u) == 2u) ? (1 << 28) : -1; h.t = 5.0f; h.u = h.v = 0.0f; h.surf = h.dp = -1;
-                if (false)
-#endif
-                if (nlist >= 0) closest_list(L, list, nlist, ro, rd, h, cand);
-                else if (kPixPacket) closest_w<SCN>(P, L, ro, rd, h, cand);
-                else if (cand) closest_l<SCN>(P, L, ro, rd, h);
-                if (cand) {
-                    obj = surface_l<SCN>(L, ro, rd, h, S);
-                    kind = obj < 0 ? 0 : (L.obj[obj].light >= 0 ? 1 : 2);
-                }
+            if (nlist >= 0) closest_list(L, list, nlist, ro, rd, h, cand);
+            else if (kPixPacket) closest_w<SCN>(P, L, ro, rd, h, cand);
+            else if (cand) closest_l<SCN>(P, L, ro, rd, h);
+            if (cand) {
+                obj = surface_l<SCN>(L, ro, rd, h, S);
+                kind = obj < 0 ? 0 : (L.obj[obj].light >= 0 ? 1 : 2);
             }
             // the chain through the window (scalar): from candidate 0 (the next sample), a
             // sample at candidate q moves to q + 1, or to q + 1 + NLD after a surface hit
@@ -269,71 +387,43 @@ __global__ __launch_bounds__(kPixBlock, XRT_PIX_WAVES) void k_pixel(KParams P, u
                 }
             }
             const bool member = (M >> lane) & 1ull;
-            v3 rad = mk(0, 0, 0);
-            if (INTEG == XRT_INTEGRATOR_DIRECT) {
-                // DirectIntegrator::integrate (Src/integrator.h:82-119); the light loop runs on
-                // every lane (the shadow trace is a wave walk), shading where a sample hit a surface
-#ifdef XRT_PIX_EXP_NOSHADE
-                const bool shade = false;
-#else
+            if constexpr (DEFER) {
+                // the window's samples as pending codes, its surface hits as queue items
                 const bool shade = member && kind == 2;
-#endif
-                if (member && kind == 0) rad = mk((float)0.18, (float)0.18, (float)0.18);
-                if (member && kind == 1) rad = light_Le(L.light[L.obj[obj].light], S.ns, rd);
-                for (int l = 0; l < P.n_lights; ++l) {
-                    v3 wi = mk(0, 0, 0), Lv = mk(0, 0, 0);
-                    float tmax = 0.0f, pdf = 0.0f;
-                    if (shade) Lv = light_sample(L.light[l], S.pos, wi, pdf, tmax, rng);
-                    const bool ray = shade && pdf != 0.0f;
-                    const float bias = 0.01f;
-                    nsh += ray ? 1u : 0u;
-                    bool vis = true;
-                    if (kPixPacket) vis = !occluded_w<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias, ray);
-                    else if (ray) vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias);
-                    if (ray) {
-                        const float cosv = smax(0.0f, dot(S.ng, wi));
-                        const v3 fr = eval_bxdf(L.obj[obj]);
-                        rad = rad + div3s(((fr * (float)vis) * Lv) * cosv, pdf);
-                    }
+                const uint64_t im = __ballot(shade);
+                if (member) {
+                    uint32_t code = 0u;
+                    if (kind == 1) code = dot(rd, S.ns) < 0.0f ? 1u + (uint32_t)L.obj[obj].light : 255u;   // light_Le
+                    if (shade) code = 128u + qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
+                    codes[pn + __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u))] = (uint8_t)code;
                 }
-            } else if (member && obj >= 0) {
-                rad = normal_color(S.ns);   // NormalIntegrator::integrate (Src/integrator.h:28-37)
-            }
-            // integrate(...) / pdf (pinhole pdf 1) and the invalid-radiance check
-            // (Src/renderer.cpp:53-73), then addPixel in sample order
-            const v3 r = rad / 1.0f;
-            const bool bad = __builtin_isnan(r.x) || __builtin_isnan(r.y) || __builtin_isnan(r.z) ||
-                             __builtin_isinf(r.x) || __builtin_isinf(r.y) || __builtin_isinf(r.z) || r.x < 0.0f ||
-                             r.y < 0.0f || r.z < 0.0f;
-            const uint64_t vm = __ballot(member && !bad);
-            nrej += (uint32_t)(__builtin_popcountll(M) - __builtin_popcountll(vm));
-            if (member && !bad) {
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(vm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)vm, 0u));
-                sum[rank] = r.x, sum[kPixSumStride + rank] = r.y, sum[2 * kPixSumStride + rank] = r.z;
-            }
-            wave_sync();
-#ifdef XRT_PIX_EXP_NOSUM
-            if (false) {
-#else
-            if (lane < 3) {
-#endif
-                const f4* q4 = reinterpret_cast<const f4*>(sum + kPixSumStride * lane);
-                const uint32_t nv = (uint32_t)__builtin_popcountll(vm);
-                for (uint32_t j = 0; j < nv; j += 8) {
-                    const f4 a = q4[j / 4], b = q4[j / 4 + 1];
-                    acc = acc + a.x;
-                    if (j + 1 < nv) acc = acc + a.y;
-                    if (j + 2 < nv) acc = acc + a.z;
-                    if (j + 3 < nv) acc = acc + a.w;
-                    if (j + 4 < nv) acc = acc + b.x;
-                    if (j + 5 < nv) acc = acc + b.y;
-                    if (j + 6 < nv) acc = acc + b.z;
-                    if (j + 7 < nv) acc = acc + b.w;
+                if (shade) {
+                    const uint32_t at = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
+                    it_i[at] = ci, it_t[at] = h.t, it_c[at] = h.code;
                 }
+                qn += (uint32_t)__builtin_popcountll(im);
+                pn += cnt, ++pw;
+                k += cnt;
+                o += 2u * pos;
+                wave_sync();
+                if (pw == 3u || qn + per_window > 64u || k >= P.spp) flush();
+            } else {
+                v3 rad = mk(0, 0, 0);
+                if (INTEG == XRT_INTEGRATOR_DIRECT) {
+                    // DirectIntegrator::integrate (Src/integrator.h:82-119)
+                    if (member && kind == 0) rad = mk((float)0.18, (float)0.18, (float)0.18);
+                    if (member && kind == 1) rad = light_Le(L.light[L.obj[obj].light], S.ns, rd);
+                    direct_light(member && kind == 2, S, obj, rng, rad);
+                } else if (member && obj >= 0) {
+                    rad = normal_color(S.ns);   // NormalIntegrator::integrate (Src/integrator.h:28-37)
+                }
+                const v3 r = rad / 1.0f;
+                const uint64_t vm = __ballot(member && !invalid(r));
+                nrej += (uint32_t)(__builtin_popcountll(M) - __builtin_popcountll(vm));
+                add_in_order(vm, r);
+                k += cnt;
+                o += 2u * pos;
             }
-            wave_sync();   // the buffer is rewritten by the next window
-            k += cnt;
-            o += 2u * pos;
         }
         if (lane < 3) px[lane] = acc;
         // the pixel's counters, as the per-slot schedules leave them for k_finish: one
@@ -363,22 +453,27 @@ bool use_pixel(const KParams& P) {
     return one_hit(P.integrator) && step_lds_bytes(P) != 0 && pix_lds_bytes(P) <= kPixLds;
 }
 
-size_t pix_lds_bytes(const KParams& P) { return pix_wave_off(P) + (size_t)(kPixBlock / 64) * kPixWaveLds; }
+size_t pix_lds_bytes(const KParams& P) {
+    const bool defer = pix_defer_rt(P);
+    const uint32_t bs = defer ? 1024u : (uint32_t)kPixBlock;
+    return pix_wave_off(P) + (size_t)(bs / 64) * (defer ? kPixWaveDeferLds : kPixWaveLds);
+}
 
 template <int SCN, int INTEG>
 static hipError_t pixel_i(const KParams& P, uint32_t* work, hipStream_t st) {
+    constexpr int BS = pix_block(SCN, INTEG);
     const size_t lds = pix_lds_bytes(P);
-    auto kern = k_pixel<SCN, INTEG>;
+    auto kern = k_pixel<SCN, INTEG, BS>;
     // persistent grid: as many blocks as fit on the device at once (LDS and VGPR bound), at
     // most one wave per pixel
     int dev = 0, ncu = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kPixBlock, lds);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BS, lds);
     if (e != hipSuccess) return e;
-    const uint64_t want = ((uint64_t)P.n_slots + kPixBlock / 64 - 1) / (kPixBlock / 64);
+    const uint64_t want = ((uint64_t)P.n_slots + BS / 64 - 1) / (BS / 64);
     const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(1, per_cu) * ncu, want));
-    hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(kPixBlock), lds, st, P, work);
+    hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(BS), lds, st, P, work);
     return hipGetLastError();
 }
 

@@ -42,6 +42,9 @@
 #ifndef XRT_PIX_FRUSTUM_MAX
 #define XRT_PIX_FRUSTUM_MAX 8192   // sphere scenes up to this size: per-pixel camera-frustum sphere lists (0: off)
 #endif
+#ifndef XRT_PIX_DEFER
+#define XRT_PIX_DEFER 1      // Direct on sphere scenes: queue the surface hits, shade three windows' worth at once
+#endif
 #ifndef XRT_PIX_PACKET
 #define XRT_PIX_PACKET 1     // traces walk the scene once per wave (coherent rays), not once per lane
 #endif
