@@ -138,19 +138,22 @@ __device__ int pix_frustum(const KParams& P, const LScene& L, uint32_t col, uint
 }
 
 // Scene::intersect over a pixel's frustum list (pix_frustum): the (t, index) minimum over the
-// listed spheres, as sphere_bvh's
-__device__ __forceinline__ void closest_list(const LScene& L, const uint16_t* list, int nlist, v3 o, v3 d, HitRec& h,
-                                             bool active) {
+// listed spheres, as sphere_bvh's.  Lane e holds list entry e's sphere (lsph: center, radius;
+// lk: original index), broadcast to the wave one entry at a time (readlane: no memory latency
+// inside the loop).
+__device__ __forceinline__ void closest_list(f4 lsph, int lk, int nlist, v3 o, v3 d, HitRec& h, bool active) {
     h.t = kINF, h.u = h.v = 0.0f, h.code = -1, h.surf = -1, h.dp = -1, h.t1 = kINF;
     h.st = h.su = h.sv = h.du = h.dv = 0.0f;
     float bt = kINF;
     int bk = -1;
     for (int e = 0; e < nlist; ++e) {
-        const int j = wave_uniform((int)list[e]);
-        const f4 S = L.ssph[j];
-        const int k = wave_uniform(L.sbk[j]) & 0x3fffffff;
+        const v3 c = mk(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.x), e)),
+                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.y), e)),
+                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.z), e)));
+        const float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.w), e));
+        const int k = __builtin_amdgcn_readlane(lk, e);
         float t = 0.0f;
-        const bool hit = active && sphere_hit(o, d, xyz(S), S.w, t);
+        const bool hit = active && sphere_hit(o, d, c, r, t);
         const bool upd = hit && (t < bt || (t == bt && k < bk));
         bt = upd ? t : bt;
         bk = upd ? k : bk;
@@ -222,6 +225,13 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
             wave_sync();
         }
         const int nlist = frustum ? pix_frustum<SCN>(P, L, col, row, list, lane) : -1;
+        f4 lsph = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // lane e: list entry e's sphere and index
+        int lk = 0;
+        if (lane < nlist) {
+            const int j = list[lane];
+            lsph = L.ssph[j];
+            lk = L.sbk[j] & 0x3fffffff;
+        }
         float* px = P.fb + 3 * ((size_t)col + (size_t)P.width * row);
         float acc = lane < 3 ? px[lane] : 0.0f;   // lane c < 3: channel c of the running sum
         uint32_t o = kMT, g = kMT, k = 0;        // next draw x[o]; x[0 .. g) generated
@@ -345,7 +355,7 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 const float v = div_h(P, (float)(int)row + rng.next());
                 camera_ray(P, u, v, ro, rd);
             }
-            if (nlist >= 0) closest_list(L, list, nlist, ro, rd, h, cand);
+            if (nlist >= 0) closest_list(lsph, lk, nlist, ro, rd, h, cand);
             else if (kPixPacket) closest_w<SCN>(P, L, ro, rd, h, cand);
             else if (cand) closest_l<SCN>(P, L, ro, rd, h);
             if (cand) {
