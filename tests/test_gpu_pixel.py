@@ -181,6 +181,30 @@ def test_deferred_shading_rejects_and_accumulate(renderer):
         assert st["rejected"] > 0
 
 
+@pytest.mark.parametrize("light", ["quad", "triangle", "sphere"])
+def test_shadow_occluder_lists(renderer, light):
+    """Direct on a sphere scene with one light traces a pixel's shadow rays against the
+    occluders that meet the hull of its camera-list spheres and the light's bounding ball
+    (pix_shadow_list) instead of walking the BVH: a grid of spheres under a quad, a triangle
+    and a sphere light, at sizes where pixels see 1-4 spheres (lists) and more (BVH walks)."""
+    s = scenes.SceneBundle()
+    for k in range(48):
+        x, z = -3.5 + (k % 8) * 1.0, -2.0 - (k // 8) * 1.0
+        s.add_sphere(f"s{k:02d}", (x, 0.1 * (k % 3), z), 0.45, (0.6, 0.6, 0.6))
+    if light == "quad":
+        s.add_quad_light("L", (-1.0, 4.0, -3.0), (1.0, 4.0, -3.0), (-1.0, 4.0, -5.0), (12.0, 12.0, 12.0))
+    elif light == "triangle":
+        s.add_triangle_light("L", (-1.0, 4.0, -3.0), (1.5, 4.0, -3.5), (0.0, 4.5, -6.0), (12.0, 9.0, 6.0))
+    else:
+        s.add_sphere_light("L", (0.5, 4.0, -4.0), 0.8, (15.0, 15.0, 15.0))
+    s.flatten()
+    for w, h in ((48, 27), (13, 7)):
+        s.camera = scenes.pinhole((1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 2.5, 3, 1), 60.0, w, h)
+        img, ref, st, g = render_pixel(renderer, s, w, h, 70, integrator="direct")
+        compare(img, ref)
+        counters_equal(g, st)
+
+
 def test_shards_and_step_schedule_agree(renderer):
     """Row shards of the pixel schedule reassemble the whole frame bit for bit, and the
     per-slot fused schedule (XRT_FLAG_NO_PIXEL) renders the same image."""

@@ -50,6 +50,7 @@ constexpr uint32_t kPixWaveLds = (kMT + 3 * kPixSumStride) * 4 + kPixList * 2;  
 constexpr uint32_t kPixFrustumMax = XRT_PIX_FRUSTUM_MAX;   // sphere scenes up to this size build the lists
 
 constexpr bool kPixPacket = XRT_PIX_PACKET != 0;   // wave-uniform scene walks (lscene.h closest_w)
+constexpr bool kPixShadowList = XRT_PIX_SHADOW_LIST != 0;   // per-pixel shadow-ray occluder lists
 
 // the words generated per chunk: one pair per lane
 constexpr uint32_t kPixChunk = 128;
@@ -123,7 +124,7 @@ __device__ int pix_frustum(const KParams& P, const LScene& L, uint32_t col, uint
         const int j = base + lane;
         bool in = false;
         if (j < P.n_sph) {
-            const f4 S = L.ssph[j];
+            const f4 S = lds4(L.ssph, j);
             const v3 c = xyz(S) - o;
             const float rr = -(__builtin_fabsf(S.w) + P.sph_pad);
             in = dot(n[0], c) >= rr && dot(n[1], c) >= rr && dot(n[2], c) >= rr && dot(n[3], c) >= rr;
@@ -159,6 +160,100 @@ __device__ __forceinline__ void closest_list(f4 lsph, int lk, int nlist, v3 o, v
         bk = upd ? k : bk;
     }
     if (bk >= 0) h.t = bt, h.code = (1 << 28) | bk;
+}
+
+// Shadow-ray occluder lists (Direct on sphere-BVH scenes with one area light).  A shadow ray
+// of the pixel starts at S.pos + 0.01 ng, S.pos within float error of a sphere s its camera
+// rays can hit (a frustum-list sphere), and runs tmax - 0.01 along wi towards a light sample
+// point p (within float error of the light), ending within 0.02 of p: so the whole segment
+// lies in the convex hull of the ball around s (radius |r_s| + 0.01 + margin) and the light's
+// bounding ball (+ 0.02 + margin).  A sphere whose occlusion test reports a hit has the hit
+// point on that segment within float error of its surface, so its ball (|r| + sph_pad) meets
+// that hull.  The hull of two balls is {x : min_s |x - a - s u| - ra - s (rb - ra) <= 0}
+// (a convex function of s); ball_meets_hull lower-bounds the minimum by the tangent at the
+// closed-form minimiser (convexity), so the test never drops a sphere that meets the hull.
+__device__ __forceinline__ bool ball_meets_hull(v3 c, float rho, v3 a, float ra, v3 b, float rb) {
+    const v3 u = b - a, w = c - a;
+    const float L2 = dot(u, u), L = __builtin_sqrtf(L2), D = rb - ra;
+    if (!(L > __builtin_fabsf(D)) || !(L2 > 0.0f)) return true;   // one ball inside the other: keep
+    const float t0 = dot(w, u) / L2;
+    const float h = length(w - u * t0);
+    float s = t0 + D * h / (L * __builtin_sqrtf(L2 - D * D));
+    s = s < 0.0f ? 0.0f : (s > 1.0f ? 1.0f : s);
+    const v3 q = w - u * s;
+    const float dq = length(q);
+    if (!(dq > 1e-6f * (L + length(w)))) return true;   // at the axis: the tangent is undefined, keep
+    const float f = dq - (ra + s * D);
+    const float fp = -dot(u, q) / dq - D;   // f'(s)
+    const float lb = f - __builtin_fabsf(fp) * (s > 0.5f ? s : 1.0f - s);
+    return lb <= rho + 1e-4f * (L + length(w)) + 1e-4f;   // + the float slack of the evaluation
+}
+
+// Every occluder sphere that meets the hull of one of the pixel's camera-list spheres and the
+// light's bounding ball, into `list` (each lane tests 1/64 of the spheres); returns the count,
+// or -1 when it overflows kPixList (the pixel's shadow rays then walk the BVH).  lsph: lane e
+// holds camera-list sphere e (nlist of them).  Every lane must call it.
+__device__ int pix_shadow_list(const KParams& P, const LScene& L, f4 lsph, int nlist, uint16_t* list, int lane) {
+    const DLight& lt = L.light[0];
+    v3 lc;
+    float lr;
+    if (lt.kind == 2) {
+        lc = ld3(lt.center), lr = __builtin_fabsf(lt.radius);
+    } else {   // quad / triangle: the centroid of its corners and the farthest corner
+        const v3 v0 = ld3(lt.v0), e1 = ld3(lt.e1), e2 = ld3(lt.e2);
+        const v3 cs[4] = {v0, v0 + e1, v0 + e2, v0 + e1 + e2};
+        const int nc = lt.kind == 0 ? 4 : 3;
+        lc = mk(0, 0, 0);
+        for (int q = 0; q < nc; ++q) lc = lc + cs[q];
+        lc = lc / (float)nc;
+        lr = 0.0f;
+        for (int q = 0; q < nc; ++q) lr = smax(lr, length(cs[q] - lc));
+        lr = lr * 1.001f;
+    }
+    const float pad = P.sph_pad;
+    lr = lr + 0.02f + pad;
+    uint32_t cnt = 0;
+    for (int base = 0; base < P.n_sph; base += 64) {
+        const int j = base + lane;
+        bool in = false;
+        if (j < P.n_sph && (ldsi(L.sbk, j) & (1 << 30))) {   // occluders only (Scene::occluded skips lights)
+            const f4 S = lds4(L.ssph, j);
+            const float rho = __builtin_fabsf(S.w) + pad;
+            for (int e = 0; e < nlist && !in; ++e) {
+                const v3 c = mk(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.x), e)),
+                                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.y), e)),
+                                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.z), e)));
+                const float r = __builtin_fabsf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.w), e))) +
+                                0.01f + pad;
+                // the hull's bounding box (grown by rho) first: most spheres are far from it
+                const v3 lo = mk(smin(c.x - r, lc.x - lr), smin(c.y - r, lc.y - lr), smin(c.z - r, lc.z - lr));
+                const v3 hi = mk(smax(c.x + r, lc.x + lr), smax(c.y + r, lc.y + lr), smax(c.z + r, lc.z + lr));
+                const bool near = S.x >= lo.x - rho && S.x <= hi.x + rho && S.y >= lo.y - rho && S.y <= hi.y + rho &&
+                                  S.z >= lo.z - rho && S.z <= hi.z + rho;
+                in = near && ball_meets_hull(xyz(S), rho, c, r, lc, lr);
+            }
+        }
+        const uint64_t mk_ = __ballot(in);
+        const uint32_t at = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk_ >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk_, 0u));
+        if (in && at < kPixList) list[at] = (uint16_t)j;
+        cnt += (uint32_t)__builtin_popcountll(mk_);
+    }
+    wave_sync();
+    return cnt <= kPixList ? (int)cnt : -1;
+}
+
+// Scene::occluded over a pixel's shadow list: lane e holds occluder e (center, radius)
+__device__ __forceinline__ bool occluded_list(f4 ssph, int nsl, v3 o, v3 d, float tmax, bool active) {
+    bool occ = false;
+    for (int e = 0; e < nsl; ++e) {
+        const v3 c = mk(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(ssph.x), e)),
+                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ssph.y), e)),
+                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ssph.z), e)));
+        const float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ssph.w), e));
+        float t = 0.0f;
+        occ = occ || (active && sphere_hit(o, d, c, r, t) && t < tmax);
+    }
+    return occ;
 }
 
 // Deferred shading (Direct on sphere-BVH scenes): a window's samples that hit a surface are
@@ -203,6 +298,32 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
     uint8_t* codes = reinterpret_cast<uint8_t*>(it_c + 64);                   // pending samples
     __syncthreads();
     const bool frustum = SCN == SCN_SPHERE && L.n_snode > 0 && P.n_sph <= (int)kPixFrustumMax;
+    // sphere-BVH scenes keep the hit sphere / object tables in global memory (load_lscene):
+    // read them as such (global loads, not flat ones)
+    const bool sbvh = SCN == SCN_SPHERE && L.n_snode > 0;
+    auto surf = [&](v3 ro, v3 rd, const HitRec& h, Surf& S) -> int {
+        if (SCN == SCN_SPHERE && sbvh) {   // surface_l's sphere branch
+            S.pos = S.ng = S.ns = S.dpdu = S.dpdv = mk(0, 0, 0);
+            if (h.code < 0) return -1;
+            const int idx = h.code & 0x0fffffff;
+            S.pos = ray_at(ro, rd, h.t);
+            S.ng = normalize(ray_at(ro, rd, h.t) - xyz(glb4(P.sph, idx)));
+            S.ns = S.ng;
+            return glbv(P.sph_obj, idx) & 0x3fffffff;
+        }
+        return surface_l<SCN>(L, ro, rd, h, S);
+    };
+    static_assert(sizeof(DObj) == 32, "DObj: 8 words {kind, material, light, medium, fr[3], pad}");
+    auto obj_word = [&](int obj, int w) -> int {
+        return sbvh ? glbv(reinterpret_cast<const int*>(P.objs), 8 * obj + w)
+                    : reinterpret_cast<const int*>(L.obj)[8 * obj + w];
+    };
+    auto obj_light = [&](int obj) { return obj_word(obj, 2); };
+    auto obj_fr = [&](int obj) {   // Lambert::evaluateBxDF (eval_bxdf)
+        return obj_word(obj, 1) == 1 ? mk(__int_as_float(obj_word(obj, 4)), __int_as_float(obj_word(obj, 5)),
+                                          __int_as_float(obj_word(obj, 6)))
+                                     : mk(0, 0, 0);
+    };
     // words a surface hit draws beyond its jitter, in pairs: one pair per area light (Direct)
     const uint32_t NLD = INTEG == XRT_INTEGRATOR_DIRECT ? (uint32_t)P.n_lights : 0u;
     const uint32_t per_window = (64u + NLD) / (1u + NLD);   // most surface hits one window's chain holds
@@ -229,8 +350,16 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
         int lk = 0;
         if (lane < nlist) {
             const int j = list[lane];
-            lsph = L.ssph[j];
-            lk = L.sbk[j] & 0x3fffffff;
+            lsph = lds4(L.ssph, j);
+            lk = ldsi(L.sbk, j) & 0x3fffffff;
+        }
+        // DEFER with one light: the pixel's shadow-ray occluders (the LDS list is free again)
+        int nsl = -1;
+        f4 ssph = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (DEFER && kPixShadowList && P.n_lights == 1 && nlist >= 1 && nlist <= 4) {
+            wave_sync();   // every lane has read its camera-list entry
+            nsl = pix_shadow_list(P, L, lsph, nlist, list, lane);
+            if (lane < nsl) ssph = lds4(L.ssph, list[lane]);
         }
         float* px = P.fb + 3 * ((size_t)col + (size_t)P.width * row);
         float acc = lane < 3 ? px[lane] : 0.0f;   // lane c < 3: channel c of the running sum
@@ -268,6 +397,9 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
         // DirectIntegrator's light loop for a sample at surface S (Src/integrator.h:94-110), every
         // lane (the shadow rays are a wave walk); `shade`: this lane's sample hit a surface
         auto direct_light = [&](bool shade, const Surf& S, int obj, LdsRng& rng, v3& rad) {
+#ifdef XRT_PIX_EXP_NOSHADE
+            return;
+#endif
             for (int l = 0; l < P.n_lights; ++l) {
                 v3 wi = mk(0, 0, 0), Lv = mk(0, 0, 0);
                 float tmax = 0.0f, pdf = 0.0f;
@@ -276,11 +408,12 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 const float bias = 0.01f;
                 nsh += ray ? 1u : 0u;
                 bool vis = true;
-                if (kPixPacket) vis = !occluded_w<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias, ray);
+                if (nsl >= 0) vis = !occluded_list(ssph, nsl, S.pos + S.ng * bias, wi, tmax - bias, ray);
+                else if (kPixPacket) vis = !occluded_w<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias, ray);
                 else if (ray) vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias);
                 if (ray) {
                     const float cosv = smax(0.0f, dot(S.ng, wi));
-                    const v3 fr = eval_bxdf(L.obj[obj]);
+                    const v3 fr = obj_fr(obj);
                     rad = rad + div3s(((fr * (float)vis) * Lv) * cosv, pdf);
                 }
             }
@@ -301,7 +434,7 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 HitRec h;
                 h.t = it_t[lane], h.u = h.v = 0.0f, h.code = it_c[lane], h.surf = -1, h.dp = -1, h.t1 = kINF;
                 h.st = h.su = h.sv = h.du = h.dv = 0.0f;
-                obj = surface_l<SCN>(L, ro, rd, h, S);
+                obj = surf(ro, rd, h, S);
             }
             direct_light(act, S, obj, rng, rad);
             const v3 r = rad / 1.0f;
@@ -355,12 +488,16 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 const float v = div_h(P, (float)(int)row + rng.next());
                 camera_ray(P, u, v, ro, rd);
             }
+#ifdef XRT_PIX_EXP_NOCAM
+            h.code = (cand && (ci & 6u) == 2u) ? ((1 << 28) | lk) : -1; h.t = 5.0f; h.u = h.v = 0.0f; h.surf = h.dp = -1;
+            if (false)
+#endif
             if (nlist >= 0) closest_list(lsph, lk, nlist, ro, rd, h, cand);
             else if (kPixPacket) closest_w<SCN>(P, L, ro, rd, h, cand);
             else if (cand) closest_l<SCN>(P, L, ro, rd, h);
             if (cand) {
-                obj = surface_l<SCN>(L, ro, rd, h, S);
-                kind = obj < 0 ? 0 : (L.obj[obj].light >= 0 ? 1 : 2);
+                obj = surf(ro, rd, h, S);
+                kind = obj < 0 ? 0 : (obj_light(obj) >= 0 ? 1 : 2);
             }
             // the chain through the window (scalar): from candidate 0 (the next sample), a
             // sample at candidate q moves to q + 1, or to q + 1 + NLD after a surface hit
@@ -403,7 +540,7 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 const uint64_t im = __ballot(shade);
                 if (member) {
                     uint32_t code = 0u;
-                    if (kind == 1) code = dot(rd, S.ns) < 0.0f ? 1u + (uint32_t)L.obj[obj].light : 255u;   // light_Le
+                    if (kind == 1) code = dot(rd, S.ns) < 0.0f ? 1u + (uint32_t)obj_light(obj) : 255u;   // light_Le
                     if (shade) code = 128u + qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
                     codes[pn + __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u))] = (uint8_t)code;
                 }
@@ -422,7 +559,7 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 if (INTEG == XRT_INTEGRATOR_DIRECT) {
                     // DirectIntegrator::integrate (Src/integrator.h:82-119)
                     if (member && kind == 0) rad = mk((float)0.18, (float)0.18, (float)0.18);
-                    if (member && kind == 1) rad = light_Le(L.light[L.obj[obj].light], S.ns, rd);
+                    if (member && kind == 1) rad = light_Le(L.light[obj_light(obj)], S.ns, rd);
                     direct_light(member && kind == 2, S, obj, rng, rad);
                 } else if (member && obj >= 0) {
                     rad = normal_color(S.ns);   // NormalIntegrator::integrate (Src/integrator.h:28-37)
