@@ -220,23 +220,6 @@ __device__ __forceinline__ int hit_object(const LScene& L, const HitRec& h) {
 // call them (ballots); `active` says which lanes have a ray.
 __device__ __forceinline__ int wave_uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// Loads through the LScene's generic pointers compile to flat loads (which wait on both the
-// LDS and the vector-memory counters) where a pointer is LDS for some scenes and global for
-// others; where the caller knows the space, these say it: ds_read / global_load.
-__device__ __forceinline__ f4 lds4(const f4* p, int i) {
-    typedef float fv4 __attribute__((ext_vector_type(4)));
-    const fv4 v = ((const __attribute__((address_space(3))) fv4*)p)[i];
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ int ldsi(const int* p, int i) { return ((const __attribute__((address_space(3))) int*)p)[i]; }
-__device__ __forceinline__ f4 glb4(const f4* p, int i) {
-    typedef float fv4 __attribute__((ext_vector_type(4)));
-    const fv4 v = ((const __attribute__((address_space(1))) fv4*)p)[i];
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-template <class T>
-__device__ __forceinline__ T glbv(const T* p, int i) { return ((const __attribute__((address_space(1))) T*)p)[i]; }
-
 template <bool ANY>
 __device__ __forceinline__ bool sphere_bvh_wave(const LScene& L, v3 o, v3 d, float tmax, float& bt, int& bk,
                                                 bool active) {
@@ -244,7 +227,7 @@ __device__ __forceinline__ bool sphere_bvh_wave(const LScene& L, v3 o, v3 d, flo
     bool occ = false;
     int i = 0;
     while (i < L.n_snode) {
-        const f4 a = lds4(L.snode, 2 * i), b = lds4(L.snode, 2 * i + 1);
+        const f4 a = L.snode[2 * i], b = L.snode[2 * i + 1];
         const bool ov = active && !occ && bvh_box(a, b, o, inv, ANY ? tmax : bt);
         if (__ballot(ov) == 0ull) {
             i = wave_uniform(__float_as_int(a.w));
@@ -254,9 +237,9 @@ __device__ __forceinline__ bool sphere_bvh_wave(const LScene& L, v3 o, v3 d, flo
         if (leaf >= 0) {
             const int first = leaf & 0xffffff, end = first + (leaf >> 24);
             for (int j = first; j < end; ++j) {
-                const int kw = wave_uniform(ldsi(L.sbk, j));
+                const int kw = wave_uniform(L.sbk[j]);
                 if (ANY && !(kw & (1 << 30))) continue;
-                const f4 S = lds4(L.ssph, j);
+                const f4 S = L.ssph[j];
                 float t = 0.0f;
                 const bool hit = ov && sphere_hit(o, d, xyz(S), S.w, t);
                 if (ANY) {

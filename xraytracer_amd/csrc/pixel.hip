@@ -124,7 +124,7 @@ __device__ int pix_frustum(const KParams& P, const LScene& L, uint32_t col, uint
         const int j = base + lane;
         bool in = false;
         if (j < P.n_sph) {
-            const f4 S = lds4(L.ssph, j);
+            const f4 S = L.ssph[j];
             const v3 c = xyz(S) - o;
             const float rr = -(__builtin_fabsf(S.w) + P.sph_pad);
             in = dot(n[0], c) >= rr && dot(n[1], c) >= rr && dot(n[2], c) >= rr && dot(n[3], c) >= rr;
@@ -216,8 +216,8 @@ __device__ int pix_shadow_list(const KParams& P, const LScene& L, f4 lsph, int n
     for (int base = 0; base < P.n_sph; base += 64) {
         const int j = base + lane;
         bool in = false;
-        if (j < P.n_sph && (ldsi(L.sbk, j) & (1 << 30))) {   // occluders only (Scene::occluded skips lights)
-            const f4 S = lds4(L.ssph, j);
+        if (j < P.n_sph && (L.sbk[j] & (1 << 30))) {   // occluders only (Scene::occluded skips lights)
+            const f4 S = L.ssph[j];
             const float rho = __builtin_fabsf(S.w) + pad;
             for (int e = 0; e < nlist && !in; ++e) {
                 const v3 c = mk(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.x), e)),
@@ -298,32 +298,6 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
     uint8_t* codes = reinterpret_cast<uint8_t*>(it_c + 64);                   // pending samples
     __syncthreads();
     const bool frustum = SCN == SCN_SPHERE && L.n_snode > 0 && P.n_sph <= (int)kPixFrustumMax;
-    // sphere-BVH scenes keep the hit sphere / object tables in global memory (load_lscene):
-    // read them as such (global loads, not flat ones)
-    const bool sbvh = SCN == SCN_SPHERE && L.n_snode > 0;
-    auto surf = [&](v3 ro, v3 rd, const HitRec& h, Surf& S) -> int {
-        if (SCN == SCN_SPHERE && sbvh) {   // surface_l's sphere branch
-            S.pos = S.ng = S.ns = S.dpdu = S.dpdv = mk(0, 0, 0);
-            if (h.code < 0) return -1;
-            const int idx = h.code & 0x0fffffff;
-            S.pos = ray_at(ro, rd, h.t);
-            S.ng = normalize(ray_at(ro, rd, h.t) - xyz(glb4(P.sph, idx)));
-            S.ns = S.ng;
-            return glbv(P.sph_obj, idx) & 0x3fffffff;
-        }
-        return surface_l<SCN>(L, ro, rd, h, S);
-    };
-    static_assert(sizeof(DObj) == 32, "DObj: 8 words {kind, material, light, medium, fr[3], pad}");
-    auto obj_word = [&](int obj, int w) -> int {
-        return sbvh ? glbv(reinterpret_cast<const int*>(P.objs), 8 * obj + w)
-                    : reinterpret_cast<const int*>(L.obj)[8 * obj + w];
-    };
-    auto obj_light = [&](int obj) { return obj_word(obj, 2); };
-    auto obj_fr = [&](int obj) {   // Lambert::evaluateBxDF (eval_bxdf)
-        return obj_word(obj, 1) == 1 ? mk(__int_as_float(obj_word(obj, 4)), __int_as_float(obj_word(obj, 5)),
-                                          __int_as_float(obj_word(obj, 6)))
-                                     : mk(0, 0, 0);
-    };
     // words a surface hit draws beyond its jitter, in pairs: one pair per area light (Direct)
     const uint32_t NLD = INTEG == XRT_INTEGRATOR_DIRECT ? (uint32_t)P.n_lights : 0u;
     const uint32_t per_window = (64u + NLD) / (1u + NLD);   // most surface hits one window's chain holds
@@ -350,8 +324,8 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
         int lk = 0;
         if (lane < nlist) {
             const int j = list[lane];
-            lsph = lds4(L.ssph, j);
-            lk = ldsi(L.sbk, j) & 0x3fffffff;
+            lsph = L.ssph[j];
+            lk = L.sbk[j] & 0x3fffffff;
         }
         // DEFER with one light: the pixel's shadow-ray occluders (the LDS list is free again)
         int nsl = -1;
@@ -359,7 +333,7 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
         if (DEFER && kPixShadowList && P.n_lights == 1 && nlist >= 1 && nlist <= 4) {
             wave_sync();   // every lane has read its camera-list entry
             nsl = pix_shadow_list(P, L, lsph, nlist, list, lane);
-            if (lane < nsl) ssph = lds4(L.ssph, list[lane]);
+            if (lane < nsl) ssph = L.ssph[list[lane]];
         }
         float* px = P.fb + 3 * ((size_t)col + (size_t)P.width * row);
         float acc = lane < 3 ? px[lane] : 0.0f;   // lane c < 3: channel c of the running sum
@@ -413,7 +387,7 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 else if (ray) vis = !occluded_l<SCN>(P, L, S.pos + S.ng * bias, wi, tmax - bias);
                 if (ray) {
                     const float cosv = smax(0.0f, dot(S.ng, wi));
-                    const v3 fr = obj_fr(obj);
+                    const v3 fr = eval_bxdf(L.obj[obj]);
                     rad = rad + div3s(((fr * (float)vis) * Lv) * cosv, pdf);
                 }
             }
@@ -434,7 +408,7 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 HitRec h;
                 h.t = it_t[lane], h.u = h.v = 0.0f, h.code = it_c[lane], h.surf = -1, h.dp = -1, h.t1 = kINF;
                 h.st = h.su = h.sv = h.du = h.dv = 0.0f;
-                obj = surf(ro, rd, h, S);
+                obj = surface_l<SCN>(L, ro, rd, h, S);
             }
             direct_light(act, S, obj, rng, rad);
             const v3 r = rad / 1.0f;
@@ -496,8 +470,8 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
             else if (kPixPacket) closest_w<SCN>(P, L, ro, rd, h, cand);
             else if (cand) closest_l<SCN>(P, L, ro, rd, h);
             if (cand) {
-                obj = surf(ro, rd, h, S);
-                kind = obj < 0 ? 0 : (obj_light(obj) >= 0 ? 1 : 2);
+                obj = surface_l<SCN>(L, ro, rd, h, S);
+                kind = obj < 0 ? 0 : (L.obj[obj].light >= 0 ? 1 : 2);
             }
             // the chain through the window (scalar): from candidate 0 (the next sample), a
             // sample at candidate q moves to q + 1, or to q + 1 + NLD after a surface hit
@@ -540,7 +514,7 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 const uint64_t im = __ballot(shade);
                 if (member) {
                     uint32_t code = 0u;
-                    if (kind == 1) code = dot(rd, S.ns) < 0.0f ? 1u + (uint32_t)obj_light(obj) : 255u;   // light_Le
+                    if (kind == 1) code = dot(rd, S.ns) < 0.0f ? 1u + (uint32_t)L.obj[obj].light : 255u;   // light_Le
                     if (shade) code = 128u + qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
                     codes[pn + __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u))] = (uint8_t)code;
                 }
@@ -559,7 +533,7 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 if (INTEG == XRT_INTEGRATOR_DIRECT) {
                     // DirectIntegrator::integrate (Src/integrator.h:82-119)
                     if (member && kind == 0) rad = mk((float)0.18, (float)0.18, (float)0.18);
-                    if (member && kind == 1) rad = light_Le(L.light[obj_light(obj)], S.ns, rd);
+                    if (member && kind == 1) rad = light_Le(L.light[L.obj[obj].light], S.ns, rd);
                     direct_light(member && kind == 2, S, obj, rng, rad);
                 } else if (member && obj >= 0) {
                     rad = normal_color(S.ns);   // NormalIntegrator::integrate (Src/integrator.h:28-37)
