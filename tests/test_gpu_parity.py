@@ -457,6 +457,22 @@ def test_c5_smoke_vpt(renderer, sched):
     assert g.draws == st["draws"] and g.segments == st["segments"] and g.stalled == st["stalled"] == 0
 
 
+def test_grid_signed_zeros_and_denormals(renderer, sched):
+    """A density grid with +0 and -0 zeros mixed, a block of -0 only and a lone denormal:
+    the device's interpolation (float index path for origin 0 / power-of-two voxels, double
+    otherwise) renders as the oracle reads it."""
+    s = scenes.smoke(40, 30, n=32)
+    g = s.medium.density
+    z = g == 0.0
+    g[z & (np.indices(g.shape).sum(axis=0) % 3 == 0)] = -0.0
+    g[:8, :8, :8] = -0.0
+    g[20:28, 0:8, 0:8] = 0.0
+    g[23, 5, 6] = np.float32(1e-40)
+    img, ref, st = render_both(renderer, s, 40, 30, 4, schedule=sched)
+    compare(img, ref)
+    assert renderer.stats.draws == st["draws"]
+
+
 def test_vpt_medium_walk_suspends_and_resumes(renderer, sched):
     """Many spp per pixel forces delta-tracking walks to cross RNG refills (suspend/resume)."""
     s = scenes.smoke(12, 9, n=32)

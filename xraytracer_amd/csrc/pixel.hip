@@ -319,6 +319,10 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 if ((uint32_t)lane + 64u * k < kMT / 4) reinterpret_cast<u32x4*>(st)[lane + 64 * k] = v[k];
             wave_sync();
         }
+#ifdef XRT_PIX_EXP_LISTS2   // timing experiment: every list built twice
+        if (frustum) (void)pix_frustum<SCN>(P, L, col, row, list, lane);
+        wave_sync();
+#endif
         const int nlist = frustum ? pix_frustum<SCN>(P, L, col, row, list, lane) : -1;
         f4 lsph = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // lane e: list entry e's sphere and index
         int lk = 0;
@@ -332,6 +336,10 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
         f4 ssph = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (DEFER && kPixShadowList && P.n_lights == 1 && nlist >= 1 && nlist <= 4) {
             wave_sync();   // every lane has read its camera-list entry
+#ifdef XRT_PIX_EXP_LISTS2
+            (void)pix_shadow_list(P, L, lsph, nlist, list, lane);
+            wave_sync();
+#endif
             nsl = pix_shadow_list(P, L, lsph, nlist, list, lane);
             if (lane < nsl) ssph = L.ssph[list[lane]];
         }

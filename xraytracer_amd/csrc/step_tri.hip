@@ -207,17 +207,6 @@ __device__ __forceinline__ bool ray_tri_nb(v3 o, v3 d, v3 v0, v3 e1, v3 e2, floa
     return !rej & (t > kEPSILON);
 }
 
-// ceil(2^32 / n) for the pair split of merged_trace's triangle-major order (n = ranked rays
-// of one object, 1..64 * (1 + kMaxLights)): floor(j * magic / 2^32) = j / n for j * n < 2^32
-struct PairMagic {
-    uint32_t m[64 * (1 + kMaxLights) + 1];
-    constexpr PairMagic() : m() {
-        for (uint32_t n = 1; n <= 64u * (1u + kMaxLights); ++n)
-            m[n] = n == 1 ? 0u : (uint32_t)((0xffffffffull / n) + 1ull);
-    }
-};
-static __constant__ const PairMagic kPairMagic{};
-
 // One cooperative trace of the wave: the extension ray (closest hit, if `ext`) and the
 // pending shadow rays (any hit, bits of `shm`).  ORIG: the closest-hit key's low word is the
 // triangle's original index (the w of its third float4, KParams::stri) instead of its LDS
@@ -264,25 +253,12 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
         wave_sync();
         const uint32_t c = B.count, first = (uint32_t)B.first;
         const uint32_t pairs = tot * c;
-#if XRT_PAIR_TRIMAJOR
-        // triangle-major: consecutive lanes take consecutive rays of one triangle, so the
-        // closest-hit atomics of a pass go to different rays' records (no same-address
-        // serialisation) and the triangle's three float4 are a broadcast read
-        const uint32_t magic = kPairMagic.m[tot];
-#else
         const uint32_t magic = B.magic;
-#endif
         for (uint32_t j0 = 0; j0 < pairs; j0 += 64) {
             const uint32_t j = j0 + (uint32_t)lane;
             if (j < pairs) {
-#if XRT_PAIR_TRIMAJOR
-                const uint32_t kt = (tot == 1u) ? j : __umulhi(j, magic);
-                const uint32_t r = j - kt * tot;
-                const uint32_t k = first + kt;
-#else
                 const uint32_t r = (c == 1u) ? j : __umulhi(j, magic);
                 const uint32_t k = first + (j - r * c);
-#endif
                 const f4 A = W.ro[r];
                 const f4 D = W.rd[r];
                 const uint32_t e = __float_as_uint(D.w);

@@ -19,9 +19,6 @@
 #ifndef XRT_LIVE16
 #define XRT_LIVE16 20000     // below: 4 slots per wave (16 lanes each; group traces only)
 #endif
-#ifndef XRT_PAIR_TRIMAJOR
-#define XRT_PAIR_TRIMAJOR 0  // merged_trace pairs ordered triangle-major (rays vary fastest across lanes)
-#endif
 #ifndef XRT_STEP_WAVES
 #define XRT_STEP_WAVES 4     // min waves per SIMD of k_step_merged / k_step (<= 128 VGPRs; 3 or 5: C2 -5% / -9%)
 #endif
