@@ -119,20 +119,31 @@ __device__ int pix_frustum(const KParams& P, const LScene& L, uint32_t col, uint
         n[k] = n[k] * (s / length(n[k]));   // unit normal pointing into the pyramid
     }
     const v3 o = mk(x[12], x[13], x[14]);
+    auto meets = [&](v3 c, float rr) {
+        return dot(n[0], c) >= rr && dot(n[1], c) >= rr && dot(n[2], c) >= rr && dot(n[3], c) >= rr;
+    };
     uint32_t cnt = 0;
-    for (int base = 0; base < P.n_sph; base += 64) {
-        const int j = base + lane;
-        bool in = false;
-        if (j < P.n_sph) {
-            const f4 S = L.ssph[j];
-            const v3 c = xyz(S) - o;
-            const float rr = -(__builtin_fabsf(S.w) + P.sph_pad);
-            in = dot(n[0], c) >= rr && dot(n[1], c) >= rr && dot(n[2], c) >= rr && dot(n[3], c) >= rr;
+    // blocks of 64 spheres (KParams::sblk) whose ball meets the pyramid, then their members
+    const int nblk = (P.n_sph + 63) >> 6;
+    for (int b0 = 0; b0 < nblk; b0 += 64) {
+        bool bin = false;
+        if (b0 + lane < nblk) {
+            const f4 B = P.sblk[b0 + lane];
+            const v3 c = xyz(B) - o;
+            bin = !XRT_PIX_BLOCKS || meets(c, -(B.w + 1e-5f * length(c)));   // + the float slack of the block's dot products
         }
-        const uint64_t mk_ = __ballot(in);
-        const uint32_t at = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk_ >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk_, 0u));
-        if (in && at < kPixList) list[at] = (uint16_t)j;
-        cnt += (uint32_t)__builtin_popcountll(mk_);
+        for (uint64_t bm = __ballot(bin); bm; bm &= bm - 1ull) {
+            const int j = ((b0 + __builtin_ctzll(bm)) << 6) + lane;
+            bool in = false;
+            if (j < P.n_sph) {
+                const f4 S = L.ssph[j];
+                in = meets(xyz(S) - o, -(__builtin_fabsf(S.w) + P.sph_pad));
+            }
+            const uint64_t mk_ = __ballot(in);
+            const uint32_t at = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk_ >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk_, 0u));
+            if (in && at < kPixList) list[at] = (uint16_t)j;
+            cnt += (uint32_t)__builtin_popcountll(mk_);
+        }
     }
     wave_sync();
     return cnt <= kPixList ? (int)cnt : -1;
@@ -212,31 +223,46 @@ __device__ int pix_shadow_list(const KParams& P, const LScene& L, f4 lsph, int n
     }
     const float pad = P.sph_pad;
     lr = lr + 0.02f + pad;
-    uint32_t cnt = 0;
-    for (int base = 0; base < P.n_sph; base += 64) {
-        const int j = base + lane;
+    // does the ball (p, rho) meet the hull of camera-list sphere e's ball and the light's?
+    auto meets = [&](v3 p, float rho) {
         bool in = false;
-        if (j < P.n_sph && (L.sbk[j] & (1 << 30))) {   // occluders only (Scene::occluded skips lights)
-            const f4 S = L.ssph[j];
-            const float rho = __builtin_fabsf(S.w) + pad;
-            for (int e = 0; e < nlist && !in; ++e) {
-                const v3 c = mk(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.x), e)),
-                                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.y), e)),
-                                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.z), e)));
-                const float r = __builtin_fabsf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.w), e))) +
-                                0.01f + pad;
-                // the hull's bounding box (grown by rho) first: most spheres are far from it
-                const v3 lo = mk(smin(c.x - r, lc.x - lr), smin(c.y - r, lc.y - lr), smin(c.z - r, lc.z - lr));
-                const v3 hi = mk(smax(c.x + r, lc.x + lr), smax(c.y + r, lc.y + lr), smax(c.z + r, lc.z + lr));
-                const bool near = S.x >= lo.x - rho && S.x <= hi.x + rho && S.y >= lo.y - rho && S.y <= hi.y + rho &&
-                                  S.z >= lo.z - rho && S.z <= hi.z + rho;
-                in = near && ball_meets_hull(xyz(S), rho, c, r, lc, lr);
-            }
+        for (int e = 0; e < nlist && !in; ++e) {
+            const v3 c = mk(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.x), e)),
+                            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.y), e)),
+                            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.z), e)));
+            const float r = __builtin_fabsf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lsph.w), e))) +
+                            0.01f + pad;
+            // the hull's bounding box (grown by rho) first: most spheres are far from it
+            const v3 lo = mk(smin(c.x - r, lc.x - lr), smin(c.y - r, lc.y - lr), smin(c.z - r, lc.z - lr));
+            const v3 hi = mk(smax(c.x + r, lc.x + lr), smax(c.y + r, lc.y + lr), smax(c.z + r, lc.z + lr));
+            const bool near = p.x >= lo.x - rho && p.x <= hi.x + rho && p.y >= lo.y - rho && p.y <= hi.y + rho &&
+                              p.z >= lo.z - rho && p.z <= hi.z + rho;
+            in = near && ball_meets_hull(p, rho, c, r, lc, lr);
         }
-        const uint64_t mk_ = __ballot(in);
-        const uint32_t at = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk_ >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk_, 0u));
-        if (in && at < kPixList) list[at] = (uint16_t)j;
-        cnt += (uint32_t)__builtin_popcountll(mk_);
+        return in;
+    };
+    uint32_t cnt = 0;
+    // blocks of 64 spheres (KParams::sblk; each member's ball lies in the block's) whose ball
+    // meets a hull, then their occluders
+    const int nblk = (P.n_sph + 63) >> 6;
+    for (int b0 = 0; b0 < nblk; b0 += 64) {
+        bool bin = false;
+        if (b0 + lane < nblk) {
+            const f4 B = P.sblk[b0 + lane];
+            bin = !XRT_PIX_BLOCKS || meets(xyz(B), B.w);
+        }
+        for (uint64_t bm = __ballot(bin); bm; bm &= bm - 1ull) {
+            const int j = ((b0 + __builtin_ctzll(bm)) << 6) + lane;
+            bool in = false;
+            if (j < P.n_sph && (L.sbk[j] & (1 << 30))) {   // occluders only (Scene::occluded skips lights)
+                const f4 S = L.ssph[j];
+                in = meets(xyz(S), __builtin_fabsf(S.w) + pad);
+            }
+            const uint64_t mk_ = __ballot(in);
+            const uint32_t at = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk_ >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk_, 0u));
+            if (in && at < kPixList) list[at] = (uint16_t)j;
+            cnt += (uint32_t)__builtin_popcountll(mk_);
+        }
     }
     wave_sync();
     return cnt <= kPixList ? (int)cnt : -1;

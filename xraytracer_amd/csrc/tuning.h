@@ -48,6 +48,9 @@
 #ifndef XRT_PIX_SHADOW_LIST
 #define XRT_PIX_SHADOW_LIST 1   // Direct, sphere scenes, one light: per-pixel shadow-ray occluder lists
 #endif
+#ifndef XRT_PIX_BLOCKS
+#define XRT_PIX_BLOCKS 1     // k_pixel list scans skip 64-sphere blocks whose ball misses (KParams::sblk)
+#endif
 #ifndef XRT_PIX_PACKET
 #define XRT_PIX_PACKET 1     // traces walk the scene once per wave (coherent rays), not once per lane
 #endif

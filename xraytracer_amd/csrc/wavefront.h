@@ -206,6 +206,7 @@ struct KParams {
     const int* sbk;           // per ssph entry: original sphere index | (occluder << 30)
     int n_snode;
     float sph_pad;            // the sphere BVH's box margin (1e-4 scene diagonal + 1e-4)
+    const f4* sblk;           // per 64 ssph entries: a ball (center, radius) holding each member's ball of radius |r| + sph_pad
     int n_segs, n_lights, n_tris, n_sph, n_box, scene_kind, n_objs, small_tri;
     int det_bounded;   // every triangle has |e1| |e2| < 2^120 (ray_tri_nb's Newton reciprocal, xrt_api.cpp)
     DMedium medium;

@@ -43,7 +43,7 @@ struct xrt_ctx {
     // scene
     std::vector<DevBuf*> scene_bufs;
     DevBuf tri, tri_ng, tri_nrm, sph, sph_obj, box, objs, lights, segs, density, obj_box, obj_plane, bvh_node,
-        bvh_tri, snode, ssph, sbk, stri, sbox, splane, bvh4;
+        bvh_tri, snode, ssph, sbk, sblk, stri, sbox, splane, bvh4;
     KParams base{};
     StepObjs step_objs{};   // kernel-argument object records of the merged-trace schedule
     StepObjs sstep{};       // two-level trace: the small objects' records (KParams::sstep)
@@ -239,7 +239,7 @@ void xrt_destroy(xrt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->tri, &c->tri_ng, &c->tri_nrm, &c->sph, &c->sph_obj, &c->box, &c->objs, &c->lights,
-                     &c->segs, &c->density, &c->obj_box, &c->obj_plane, &c->bvh_node, &c->bvh_tri, &c->snode, &c->ssph, &c->sbk, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
+                     &c->segs, &c->density, &c->obj_box, &c->obj_plane, &c->bvh_node, &c->bvh_tri, &c->snode, &c->ssph, &c->sbk, &c->sblk, &c->ray_o, &c->ray_d, &c->thr, &c->rad, &c->thr_prev, &c->hit,
                      &c->hit2, &c->hit3, &c->sh_o, &c->sh_d, &c->sh_c, &c->med, &c->med2, &c->nee, &c->state,
                      &c->sample_k, &c->depth, &c->occ, &c->rng_c, &c->rng_g, &c->ring, &c->c_seg, &c->c_shadow,
                      &c->c_rej, &c->c_stall, &c->lists, &c->counts, &c->stats, &c->fb, &c->scratch, &c->kparams};
@@ -574,11 +574,34 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
             bs[i] = sph[k];
             bk[i] = (int)k | (sph_obj[k] & (1 << 30));
         }
+        // a ball around every 64 consecutive spheres of the leaf order (spatially coherent
+        // blocks): it contains each member's ball of radius |r| + sph_pad, so the pixel
+        // schedule's list scans skip a block whose ball misses the region (pixel.hip)
+        std::vector<f4> blk((ns + 63) / 64);
+        for (size_t b = 0; b < blk.size(); ++b) {
+            const size_t i0 = 64 * b, i1 = std::min(ns, i0 + 64);
+            double lo3[3] = {1e300, 1e300, 1e300}, hi3[3] = {-1e300, -1e300, -1e300};
+            for (size_t i = i0; i < i1; ++i)
+                for (int q = 0; q < 3; ++q) {
+                    const double cq = q == 0 ? bs[i].x : q == 1 ? bs[i].y : bs[i].z;
+                    lo3[q] = std::min(lo3[q], cq), hi3[q] = std::max(hi3[q], cq);
+                }
+            const double C[3] = {0.5 * (lo3[0] + hi3[0]), 0.5 * (lo3[1] + hi3[1]), 0.5 * (lo3[2] + hi3[2])};
+            const float Cf[3] = {(float)C[0], (float)C[1], (float)C[2]};
+            double R = 0.0;
+            for (size_t i = i0; i < i1; ++i) {
+                const double dx = (double)bs[i].x - Cf[0], dy = (double)bs[i].y - Cf[1], dz = (double)bs[i].z - Cf[2];
+                R = std::max(R, std::sqrt(dx * dx + dy * dy + dz * dz) + std::fabs((double)bs[i].w));
+            }
+            blk[b] = f4{Cf[0], Cf[1], Cf[2], (float)(R * (1.0 + 1e-5)) + P.sph_pad};
+        }
         if ((rc = upload(c, c->snode, T.data(), T.size() * sizeof(SkipNode))) ||
             (rc = upload(c, c->ssph, bs.data(), bs.size() * sizeof(f4))) ||
-            (rc = upload(c, c->sbk, bk.data(), bk.size() * sizeof(int))))
+            (rc = upload(c, c->sbk, bk.data(), bk.size() * sizeof(int))) ||
+            (rc = upload(c, c->sblk, blk.data(), blk.size() * sizeof(f4))))
             return rc;
         P.snode = as<f4>(c->snode), P.ssph = as<f4>(c->ssph), P.sbk = as<int>(c->sbk);
+        P.sblk = as<f4>(c->sblk);
         P.n_snode = (int)T.size();
     }
     c->obj_tri_first = std::move(tri_first);
