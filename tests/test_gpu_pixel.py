@@ -106,6 +106,37 @@ def test_frustum_lists_and_their_overflow(renderer, wh):
     counters_equal(g, st)
 
 
+def far_cluster(w, h, n=300, seed=11):
+    """n small spheres in a 12-unit cluster around (5000, 2000, -8000) with a sphere light and
+    the camera 15 units away: coordinates ~1e4 against a ~20-unit scene, so the float error of
+    the list tests' dot products is a few times 1e-4, near the BVH margin (sph_pad)."""
+    rng = np.random.default_rng(seed)
+    s = scenes.SceneBundle()
+    base = np.array([5000.0, 2000.0, -8000.0])
+    for k in range(n):
+        c = base + rng.uniform(-6.0, 6.0, 3)
+        s.add_sphere(f"s{k:03d}", tuple(float(x) for x in c), float(rng.uniform(0.2, 0.6)),
+                     tuple(float(x) for x in rng.uniform(0.2, 0.9, 3)))
+    s.add_sphere_light("SphereLight", tuple(float(x) for x in base + [0.0, 12.0, 0.0]), 2.0, (30.0, 30.0, 30.0))
+    s.flatten()
+    s.camera = scenes.pinhole((1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, base[0], base[1] + 1.0, base[2] + 15.0, 1), 50.0, w, h)
+    s.integrator, s.max_depth = "direct", 1
+    return s
+
+
+@pytest.mark.parametrize("wh", [(40, 30), (160, 90)])
+def test_block_culled_lists_far_from_origin(renderer, wh):
+    """The frustum and shadow lists are built from 64-sphere blocks whose bounding ball meets
+    the pixel's pyramid / the shadow hulls (KParams::sblk): a cluster far from the origin (float
+    error of the tests near the margin) with 5 blocks, at a coarse and a fine pixel size."""
+    w, h = wh
+    s = far_cluster(w, h)
+    img, ref, st, g = render_pixel(renderer, s, w, h, 48)
+    compare(img, ref)
+    counters_equal(g, st)
+    assert st["shadow_rays"] > 0
+
+
 @pytest.mark.parametrize("spp", [1, 2, 21, 31, 32, 33, 63, 64, 65, 127, 129, 300])
 def test_window_edges_two_lights(renderer, spp):
     """Two area lights (NL = 2: a surface hit draws 4 light words, so a chain skips 2
