@@ -345,10 +345,6 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 if ((uint32_t)lane + 64u * k < kMT / 4) reinterpret_cast<u32x4*>(st)[lane + 64 * k] = v[k];
             wave_sync();
         }
-#ifdef XRT_PIX_EXP_LISTS2   // timing experiment: every list built twice
-        if (frustum) (void)pix_frustum<SCN>(P, L, col, row, list, lane);
-        wave_sync();
-#endif
         const int nlist = frustum ? pix_frustum<SCN>(P, L, col, row, list, lane) : -1;
         f4 lsph = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // lane e: list entry e's sphere and index
         int lk = 0;
@@ -362,10 +358,6 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
         f4 ssph = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (DEFER && kPixShadowList && P.n_lights == 1 && nlist >= 1 && nlist <= 4) {
             wave_sync();   // every lane has read its camera-list entry
-#ifdef XRT_PIX_EXP_LISTS2
-            (void)pix_shadow_list(P, L, lsph, nlist, list, lane);
-            wave_sync();
-#endif
             nsl = pix_shadow_list(P, L, lsph, nlist, list, lane);
             if (lane < nsl) ssph = L.ssph[list[lane]];
         }
@@ -405,9 +397,6 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
         // DirectIntegrator's light loop for a sample at surface S (Src/integrator.h:94-110), every
         // lane (the shadow rays are a wave walk); `shade`: this lane's sample hit a surface
         auto direct_light = [&](bool shade, const Surf& S, int obj, LdsRng& rng, v3& rad) {
-#ifdef XRT_PIX_EXP_NOSHADE
-            return;
-#endif
             for (int l = 0; l < P.n_lights; ++l) {
                 v3 wi = mk(0, 0, 0), Lv = mk(0, 0, 0);
                 float tmax = 0.0f, pdf = 0.0f;
@@ -496,10 +485,6 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 const float v = div_h(P, (float)(int)row + rng.next());
                 camera_ray(P, u, v, ro, rd);
             }
-#ifdef XRT_PIX_EXP_NOCAM
-            h.code = (cand && (ci & 6u) == 2u) ? ((1 << 28) | lk) : -1; h.t = 5.0f; h.u = h.v = 0.0f; h.surf = h.dp = -1;
-            if (false)
-#endif
             if (nlist >= 0) closest_list(lsph, lk, nlist, ro, rd, h, cand);
             else if (kPixPacket) closest_w<SCN>(P, L, ro, rd, h, cand);
             else if (cand) closest_l<SCN>(P, L, ro, rd, h);
