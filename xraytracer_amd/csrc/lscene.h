@@ -333,7 +333,9 @@ __host__ __device__ inline uint32_t kstep_refill_off(const KParams& P, int bs) {
 // it.  Sphere-BVH scenes keep the BVH, the spheres in leaf order and their index words in
 // LDS; the original-order sphere / object tables (read once per hit) stay in global memory.
 // Every thread of the block calls it; the caller barriers before the first trace.
-__device__ inline LScene load_lscene(const KParams& P, char* lb, int tid, int bs) {
+// bvh_lds = false (k_pixel): the sphere BVH, leaf-order spheres and index words are read
+// from global memory (L1 / L2) and take no LDS.
+__device__ inline LScene load_lscene(const KParams& P, char* lb, int tid, int bs, bool bvh_lds = true) {
     const StepLayout Lo = step_layout(P);
     LScene L;
     L.tri = reinterpret_cast<const f4*>(lb + Lo.tri);
@@ -351,7 +353,11 @@ __device__ inline LScene load_lscene(const KParams& P, char* lb, int tid, int bs
     if (P.scene_kind == SCN_TRI) lds_copy(const_cast<DObjBox*>(L.box), P.obj_box, P.n_objs, tid, bs);
     lds_copy(const_cast<f4*>(L.bx), P.box, 2 * P.n_box, tid, bs);
     lds_copy(const_cast<DLight*>(L.light), P.lights, P.n_lights, tid, bs);
-    if (P.scene_kind == SCN_SPHERE && P.n_snode > 0) {
+    if (P.scene_kind == SCN_SPHERE && P.n_snode > 0 && !bvh_lds) {
+        L.snode = P.snode, L.ssph = P.ssph, L.sbk = P.sbk;
+        L.n_snode = P.n_snode;
+        L.sph = P.sph, L.sobj = P.sph_obj, L.obj = P.objs;
+    } else if (P.scene_kind == SCN_SPHERE && P.n_snode > 0) {
         L.snode = reinterpret_cast<const f4*>(lb + Lo.snode);
         L.ssph = reinterpret_cast<const f4*>(lb + Lo.ssph);
         L.sbk = reinterpret_cast<const int*>(lb + Lo.sbk);

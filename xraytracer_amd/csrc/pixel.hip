@@ -298,13 +298,19 @@ constexpr bool pix_defer(int scn, int integ) {
 }
 constexpr uint32_t kPixPend = 192;   // pending samples of three windows (codes)
 constexpr uint32_t kPixWaveDeferLds = kPixWaveLds + 3 * kPixSumStride * 4 + 3 * 64 * 4 + kPixPend;
-constexpr int pix_block(int scn, int integ) { return pix_defer(scn, integ) ? 1024 : kPixBlock; }
+constexpr int pix_block(int scn, int integ) { return pix_defer(scn, integ) ? XRT_PIX_DEFER_BLOCK : kPixBlock; }
 __host__ __device__ inline bool pix_defer_rt(const KParams& P) {
     return XRT_PIX_DEFER && P.scene_kind == SCN_SPHERE && P.integrator == XRT_INTEGRATOR_DIRECT;
 }
 
 // LDS bytes of the pixel schedule: the scene carve, then one slice per wave
-__host__ __device__ inline uint32_t pix_wave_off(const KParams& P) { return (step_layout(P).total + 15u) & ~15u; }
+// (with XRT_PIX_GLOBAL_BVH the sphere BVH — the carve's last three regions — stays in global
+// memory: the lists hold a pixel's spheres in registers, so the BVH is read only by the list
+// scans (from L1 / L2) and by overflow pixels, and the block skips copying ~36 KB into LDS)
+__host__ __device__ inline uint32_t pix_wave_off(const KParams& P) {
+    const StepLayout Lo = step_layout(P);
+    return ((XRT_PIX_GLOBAL_BVH && P.n_snode > 0 ? Lo.snode : Lo.total) + 15u) & ~15u;
+}
 
 template <int SCN, int INTEG, int BS>
 __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t* __restrict__ work) {
@@ -313,7 +319,7 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
     extern __shared__ __attribute__((aligned(16))) f4 lds_pix[];
     char* lb = reinterpret_cast<char*>(lds_pix);
     const int tid = threadIdx.x, lane = tid & 63;
-    const LScene L = load_lscene(P, lb, tid, BS);
+    const LScene L = load_lscene(P, lb, tid, BS, !XRT_PIX_GLOBAL_BVH);
     uint32_t* st = reinterpret_cast<uint32_t*>(lb + pix_wave_off(P) + (tid >> 6) * kWave);
     float* sum = reinterpret_cast<float*>(st + kMT);
     uint16_t* list = reinterpret_cast<uint16_t*>(sum + 3 * kPixSumStride);
@@ -595,7 +601,7 @@ bool use_pixel(const KParams& P) {
 
 size_t pix_lds_bytes(const KParams& P) {
     const bool defer = pix_defer_rt(P);
-    const uint32_t bs = defer ? 1024u : (uint32_t)kPixBlock;
+    const uint32_t bs = defer ? (uint32_t)XRT_PIX_DEFER_BLOCK : (uint32_t)kPixBlock;
     return pix_wave_off(P) + (size_t)(bs / 64) * (defer ? kPixWaveDeferLds : kPixWaveLds);
 }
 

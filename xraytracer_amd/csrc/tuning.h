@@ -36,8 +36,14 @@
 #ifndef XRT_PIX_BLOCK
 #define XRT_PIX_BLOCK 512    // threads per block (8 waves share one LDS copy of the scene)
 #endif
+#ifndef XRT_PIX_GLOBAL_BVH
+#define XRT_PIX_GLOBAL_BVH 1 // k_pixel reads the sphere BVH from global memory, not an LDS copy per block (C3 -1.7%)
+#endif
+#ifndef XRT_PIX_DEFER_BLOCK
+#define XRT_PIX_DEFER_BLOCK 1024  // k_pixel threads per block, deferred-shading (C3) kernels (640 at 5 waves: C3 +18%)
+#endif
 #ifndef XRT_PIX_WAVES
-#define XRT_PIX_WAVES 4      // min waves per SIMD (<= 128 VGPRs)
+#define XRT_PIX_WAVES 4      // min waves per SIMD (<= 128 VGPRs; 5 with 640-thread blocks: C3 +18%)
 #endif
 #ifndef XRT_PIX_FRUSTUM_MAX
 #define XRT_PIX_FRUSTUM_MAX 8192   // sphere scenes up to this size: per-pixel camera-frustum sphere lists (0: off)
