@@ -230,10 +230,21 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
     for (int ob = 0; ob < n; ++ob) {
         const StepObj B = SO.o[ob];
         bool need[R];
-        need[0] = ext && !plane_away(o, d, B.axis, B.plane) && obj_overlap(oi[0], inv[0], B, kINF);
+#if XRT_TRACE_TLIM
+        // the objects so far: an extension ray skips an object whose box it enters beyond its
+        // closest hit (every triangle inside lies deeper than the box margin, far above the
+        // float error of either t; ties are still tested), a shadow ray one it is occluded by
+        const unsigned long long cur = W.best[lane];
+        const float bt = cur == ~0ull ? kINF : __uint_as_float((uint32_t)(cur >> 32));
+        const uint32_t done = W.occ[lane];
+#else
+        const float bt = kINF;
+        const uint32_t done = 0u;
+#endif
+        need[0] = ext && !plane_away(o, d, B.axis, B.plane) && obj_overlap(oi[0], inv[0], B, bt);
 #pragma unroll
         for (int l = 0; l < NL; ++l)
-            need[1 + l] = B.occluder && ((shm >> l) & 1u) && !plane_away(so[l], sd[l], B.axis, B.plane) &&
+            need[1 + l] = B.occluder && ((shm & ~done) >> l & 1u) && !plane_away(so[l], sd[l], B.axis, B.plane) &&
                           obj_overlap(oi[1 + l], inv[1 + l], B, stm[l]);
         // the rays themselves are ranked into W (not their ids), so a pair reads its ray
         // with one LDS access instead of an id and then the ray

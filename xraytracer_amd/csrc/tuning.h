@@ -19,6 +19,9 @@
 #ifndef XRT_LIVE16
 #define XRT_LIVE16 20000     // below: 4 slots per wave (16 lanes each; group traces only)
 #endif
+#ifndef XRT_TRACE_TLIM
+#define XRT_TRACE_TLIM 1     // merged_trace: cull objects beyond the ray's closest hit so far / after occlusion (C2 -1.2%)
+#endif
 #ifndef XRT_STEP_WAVES
 #define XRT_STEP_WAVES 4     // min waves per SIMD of k_step_merged / k_step (<= 128 VGPRs; 3 or 5: C2 -5% / -9%)
 #endif
