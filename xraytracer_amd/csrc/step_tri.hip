@@ -265,26 +265,36 @@ __device__ __forceinline__ void merged_trace(const StepObjs& SO, const LScene& L
         const uint32_t c = B.count, first = (uint32_t)B.first;
         const uint32_t pairs = tot * c;
         const uint32_t magic = B.magic;
-        for (uint32_t j0 = 0; j0 < pairs; j0 += 64) {
-            const uint32_t j = j0 + (uint32_t)lane;
-            if (j < pairs) {
-                const uint32_t r = (c == 1u) ? j : __umulhi(j, magic);
-                const uint32_t k = first + (j - r * c);
-                const f4 A = W.ro[r];
-                const f4 D = W.rd[r];
-                const uint32_t e = __float_as_uint(D.w);
-                float t;
-                const f4 C = L.tri[3 * k + 2];
-                const bool hit = ray_tri_nb(xyz(A), xyz(D), xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(C), t);
-                if (hit) {
-                    if (e < 64u)
-                        atomicMin(&W.best[e], ((unsigned long long)__float_as_uint(t) << 32) |
-                                                  (ORIG ? __float_as_uint(C.w) : k));
-                    else if (t < A.w)
-                        atomicOr(&W.occ[e & 63u], 1u << ((e >> 6) - 1u));
-                }
+        // one (ray, triangle) pair per lane and step: an out-of-range lane of the last step
+        // tests the last pair again with its result dropped (no divergent branch; two steps
+        // per iteration with both tests before the merges measured 5% slower on C2)
+        struct PairHit {
+            bool hit;
+            uint32_t e, idx;
+            float t, tw;
+        };
+        auto test = [&](uint32_t j) {
+            const bool valid = j < pairs;
+            const uint32_t jj = valid ? j : pairs - 1u;
+            const uint32_t r = (c == 1u) ? jj : __umulhi(jj, magic);
+            const uint32_t k = first + (jj - r * c);
+            const f4 A = W.ro[r];
+            const f4 D = W.rd[r];
+            const f4 C = L.tri[3 * k + 2];
+            PairHit p;
+            p.hit = ray_tri_nb(xyz(A), xyz(D), xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(C), p.t) && valid;
+            p.e = __float_as_uint(D.w), p.tw = A.w, p.idx = ORIG ? __float_as_uint(C.w) : k;
+            return p;
+        };
+        auto merge = [&](const PairHit& p) {
+            if (p.hit) {
+                if (p.e < 64u)
+                    atomicMin(&W.best[p.e], ((unsigned long long)__float_as_uint(p.t) << 32) | p.idx);
+                else if (p.t < p.tw)
+                    atomicOr(&W.occ[p.e & 63u], 1u << ((p.e >> 6) - 1u));
             }
-        }
+        };
+        for (uint32_t j0 = 0; j0 < pairs; j0 += 64u) merge(test(j0 + (uint32_t)lane));
         wave_sync();
     }
     best = W.best[lane];
