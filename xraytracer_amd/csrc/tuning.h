@@ -103,7 +103,7 @@
 #define XRT_VPT_EVENTS 1     // one event (a trace or one collision) per loop iteration
 #endif
 #ifndef XRT_VPT_EV_VISITS
-#define XRT_VPT_EV_VISITS 128  // ... events per slot per launch
+#define XRT_VPT_EV_VISITS 128  // ... events per slot per launch (96: C5 +1%, 150: neutral)
 #endif
 #ifndef XRT_VPT_EV_DRAWS
 #define XRT_VPT_EV_DRAWS 4   // ... draws of an event for the refill threshold (a collision draws <= 5)
