@@ -43,6 +43,7 @@
 
 namespace xrt {
 
+constexpr bool kPixStride4 = XRT_PIX_STRIDE4;   // stride-4 candidate windows after all-hit windows
 constexpr int kPixBlock = XRT_PIX_BLOCK;           // threads per block: 8 waves share one LDS scene copy
 constexpr uint32_t kPixSumStride = 68;             // ordered-sum buffer row (floats): 64 + 4, rows on other banks
 constexpr uint32_t kPixList = 64;                   // camera-frustum sphere list entries per wave (16-bit)
@@ -372,6 +373,7 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
         uint32_t o = kMT, g = kMT, k = 0;        // next draw x[o]; x[0 .. g) generated
         uint32_t nsh = 0, nrej = 0;
         uint32_t qn = 0, pn = 0, pw = 0;         // DEFER: queued items, pending samples, windows since a flush
+        bool s4next = false;                     // the next window is a stride-4 window
 
         // Image::addPixel in sample order for the lanes of vm (lane order), each with value r:
         // ranked into the sum buffer, then added one after the other by lanes 0..2 (a channel each)
@@ -470,8 +472,16 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
         while (k < P.spp) {
             const uint32_t rem = P.spp - k;
             // candidates that can lie on the chain: rem samples advance at most 1 + NLD each
+            // stride-4 windows (DEFER, one light): after a window whose samples all hit a
+            // surface, the candidates sit 4 words apart — the offsets of a run of hits — and
+            // the window ends at the first candidate that is not a hit (its successor lies
+            // between two candidates).  Queued items are flushed before and after it, so its
+            // 258 words and its items' stay within the 624-word buffer.
+            const bool s4 = DEFER && NLD == 1 && kPixStride4 && s4next && rem >= 64u;
+            if (s4 && qn) flush();
+            const uint32_t stride = s4 ? 4u : 2u;
             const uint32_t span = rem >= 64u ? 64u : min(64u, rem * (1u + NLD));
-            const uint32_t need = o + 2u * span + 2u * NLD;   // words this window may read
+            const uint32_t need = o + stride * span + 2u * NLD;   // words this window may read
             while (g < need) {
                 pix_gen(st, g, lane);
                 g += kPixChunk;
@@ -479,7 +489,7 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
             // the candidate sample at offset o + 2·lane: jitter, camera ray, Scene::intersect
             // (Src/renderer.cpp:44-53)
             const bool cand = (uint32_t)lane < span;
-            uint32_t ci = (o % kMT) + 2u * (uint32_t)lane;
+            uint32_t ci = (o % kMT) + stride * (uint32_t)lane;
             if (ci >= kMT) ci -= kMT;
             LdsRng rng{st, ci};
             v3 ro = mk(0, 0, 0), rd = mk(0, 0, 0);
@@ -502,8 +512,15 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
             // sample at candidate q moves to q + 1, or to q + 1 + NLD after a surface hit
             const uint64_t smask = NLD ? (uint64_t)__ballot(kind == 2) : 0ull;
             uint64_t M = 0;
-            uint32_t cnt = 0, pos = 0;
-            if (NLD == 1 && rem >= 64u) {
+            uint32_t cnt = 0, pos = 0;   // pos: words consumed / 2
+            if (s4) {
+                const uint64_t nh = ~smask;   // span == 64
+                const uint32_t last = nh ? (uint32_t)__builtin_ctzll(nh) : 63u;
+                M = last == 63u ? ~0ull : ((1ull << (last + 1u)) - 1ull);
+                cnt = last + 1u;
+                pos = 2u * last + (((smask >> last) & 1ull) ? 2u : 1u);
+                s4next = nh == 0ull;
+            } else if (NLD == 1 && rem >= 64u) {
                 // one light, a full window (bit-parallel): a surface-hit sample skips the next
                 // candidate, so within a run of surface hits that starts on the chain every
                 // other candidate is a sample.  kill = the surface hits on the chain: a run's
@@ -532,6 +549,7 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                     pos = q + 1u + NLD;
                 }
             }
+            if (!s4) s4next = kPixStride4 && DEFER && NLD == 1 && cnt >= 32u && (M & ~smask) == 0ull;
             const bool member = (M >> lane) & 1ull;
             if constexpr (DEFER) {
                 // the window's samples as pending codes, its surface hits as queue items
@@ -552,7 +570,8 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 k += cnt;
                 o += 2u * pos;
                 wave_sync();
-                if (pw == 3u || qn + per_window > 64u || k >= P.spp) flush();
+                // a stride-4 window spans 258 words: its items are shaded before the next window
+                if (s4 || pw == 3u || qn + (s4next ? 64u : per_window) > 64u || k >= P.spp) flush();
             } else {
                 v3 rad = mk(0, 0, 0);
                 if (INTEG == XRT_INTEGRATOR_DIRECT) {

@@ -39,6 +39,9 @@
 #ifndef XRT_PIX_BLOCK
 #define XRT_PIX_BLOCK 512    // threads per block (8 waves share one LDS copy of the scene)
 #endif
+#ifndef XRT_PIX_STRIDE4
+#define XRT_PIX_STRIDE4 1    // k_pixel (Direct, one light): 4-word candidate stride after a window of surface hits
+#endif
 #ifndef XRT_PIX_GLOBAL_BVH
 #define XRT_PIX_GLOBAL_BVH 1 // k_pixel reads the sphere BVH from global memory, not an LDS copy per block (C3 -1.7%)
 #endif
