@@ -3,8 +3,9 @@
 One step = one full frame of the workload (default C2: Cornell box 800x600, 1024 spp,
 GIIntegrator(3)), rendered by the MI355X wavefront through libxrt_hip.so with the scene
 already resident in HBM.  With N GPUs (one process per GPU) each rank renders the rows
-y % N == rank and the float3 framebuffers are summed to rank 0 with an RCCL reduce (exact:
-the other ranks contribute zeros).  Total work is fixed as N grows: "strong".  Under torchrun
+y % N == rank and rank 0 assembles the frame with one RCCL gather of every rank's packed rows
+(--assembly reduce: a SUM reduce of the zero-elsewhere framebuffers; both exact).  Total work
+is fixed as N grows: "strong".  Under torchrun
 WORLD_SIZE must equal N; without a launcher and N > 1 the bench starts N ranks itself
 (torch.distributed.run, child process); it exits non-zero rather than render N > 1 on one GPU.
 
@@ -39,6 +40,9 @@ VALU_PEAK_GINST = SIMDS * CLOCK_HZ / VALU_CYCLES / 1e9
 # schedule splits it: k_trace = extend + shadow (108·Q), k_shade = the rest.
 B_SAMPLE, B_SEGMENT, B_DRAW = 68, 264, 12
 B_TRACE_SEG = 24 + 16 + 44 + 24
+# k_pixel (Direct / Normal pixel chains) never writes path records; what it must move is each
+# pixel's seeded mt19937 state (624 words, read once) and its framebuffer pixel (read + write)
+PIX_STATE_BYTES = 624 * 4
 FLOP_PER_TRI_TEST = 40          # Moller-Trumbore arithmetic per triangle test (secondary)
 
 
@@ -171,6 +175,10 @@ def main():
     ap.add_argument("--schedule", default="auto", choices=("auto", "step", "wavefront"))
     ap.add_argument("--traffic", default=None, help="default profiles/traffic_<CONFIG>.json")
     ap.add_argument("--pmc", default=None, help="default profiles/pmc_<CONFIG>.json")
+    ap.add_argument("--assembly", default="gather", choices=("gather", "reduce"),
+                    help="N > 1: frame assembly on rank 0 — gather each rank's owned rows, or reduce(SUM) full frames")
+    ap.add_argument("--test-standin", default=None, metavar="MODULE:FACTORY",
+                    help="TESTS ONLY (tests/test_bench_launch.py): a CPU stand-in renderer instead of the HIP one")
     args = ap.parse_args()
     args.traffic = args.traffic or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     args.pmc = args.pmc or os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
@@ -178,12 +186,16 @@ def main():
     import numpy as np
     import torch
 
-    # Tests only (tests/test_bench_launch.py): XRT_BENCH_STANDIN="module:factory" swaps the
-    # HIP renderer for a CPU stand-in (not the oracle) so the multi-rank plumbing — the spawn,
-    # torch.distributed.run's rank environment, process-group init, the framebuffer reduce and
-    # the max-over-ranks timing — runs end to end on a GPU-less machine over gloo.  Read before
-    # any GPU call; the default run never sets it, and a stand-in line says so in "data".
-    standin = os.environ.get("XRT_BENCH_STANDIN")
+    # Tests only (tests/test_bench_launch.py): --test-standin MODULE:FACTORY swaps the HIP
+    # renderer for a CPU stand-in (not the oracle) so the multi-rank plumbing — the spawn,
+    # torch.distributed.run's rank environment, process-group init, the frame assembly and the
+    # max-over-ranks timing — runs end to end on a GPU-less machine over gloo.  An explicit
+    # flag (forwarded to the spawned ranks with the rest of argv), announced on stderr, and a
+    # stand-in line says so in "data".
+    standin = args.test_standin
+    if standin:
+        print(f"bench.py: WARNING: --test-standin {standin}: CPU stand-in renderer, not a measurement",
+              file=sys.stderr, flush=True)
     on_gpu = not standin
     devices = torch.cuda.device_count() if on_gpu else env_int("XRT_BENCH_STANDIN_DEVICES", 8)
     action, what = plan_launch(args.gpus, os.environ, devices)
@@ -234,11 +246,12 @@ def main():
     fb = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
     timing = not args.no_timing
 
-    sharded = distributed.ShardedRenderer(r, dist, time_reduce=True)
+    sharded = distributed.ShardedRenderer(r, dist, time_reduce=True, assembly=args.assembly)
 
     def step(timed):
-        # rank's rows, then reduce(SUM) into rank 0; the render waits for the work queued on
-        # torch's stream (the previous step's reduce) before it overwrites fb
+        # rank's rows, then the frame assembled on rank 0 (gather of the owned rows, or a
+        # reduce(SUM)); the render waits for the work queued on torch's stream (the previous
+        # step's collective) before it overwrites fb
         return sharded.render(scene, W, H, fb, timing=timing and timed, schedule=args.schedule)
 
     for _ in range(args.warmup):
@@ -301,7 +314,22 @@ def main():
             traffic = tj.get("hbm_bytes_per_launch") if tj else None
             pmc = load_keyed(args.pmc, args.config, kname)
             model = None
-            if kbytes is not None:
+            if sched == abi.XRT_SCHED_PIXEL:
+                # k_pixel keeps a pixel's whole sample chain in registers and LDS: the bytes it
+                # needs are each pixel's seeded mt19937 state (read once) and its framebuffer
+                # pixel (read, written); the scene is read into LDS per block (L2-resident)
+                kbytes = samples / SPP * (PIX_STATE_BYTES + 24)
+                per_launch = kbytes / launches
+                achieved = per_launch / avg_s / 1e9
+                model = {"what": "k_pixel required bytes: seeded mt19937 state 2,496 B + framebuffer read/write "
+                                 "24 B per pixel",
+                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "bytes_per_pixel": PIX_STATE_BYTES + 24,
+                         "algorithmic_bytes_per_launch": round(per_launch, 1),
+                         "soa_model_not_applicable": "SURVEY.md 8d's B_s = 68 + 264*Q + 12*D prices the SoA "
+                                                     "wavefront form of the path (ray, hit and shadow records "
+                                                     "per segment); k_pixel writes none of them"}
+            elif kbytes is not None:
                 per_launch = kbytes / launches
                 achieved = per_launch / avg_s / 1e9
                 model = {"what": "SURVEY.md 8d algorithmic bytes, B_s = 68 + 264*Q + 12*D per sample",
@@ -311,8 +339,9 @@ def main():
                 if model["frac"] > 1.0:
                     # the fused kernels keep path state on chip: the model's bytes are those of
                     # the SoA wavefront form of the path, not a bound on this kernel
-                    model["note"] = ("above 1: the kernel keeps the path state the model streams in registers / "
-                                     "LDS; hbm_measured is what it moves")
+                    model["applicable"] = False
+                    model["note"] = ("not applicable (frac > 1): the kernel keeps the path state the model streams "
+                                     "in registers / LDS; hbm_measured is what it moves")
             hbm = None
             if traffic:
                 hbm = {"achieved": round(traffic / avg_s / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -331,7 +360,7 @@ def main():
                 head, bound = valu, "valu"
             elif hbm:
                 head, bound = hbm, "hbm"
-            elif model:   # no counters for this build: the model figure, labelled as such
+            elif model and model.get("applicable", True):   # no counters: the model figure, labelled as such
                 head, bound = model, "hbm (model; unmeasured)"
             else:
                 head, bound = {"achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None}, "unmeasured"
@@ -364,7 +393,8 @@ def main():
                                    f"(maxDepth={cfg['max_depth']})",
                        "width": W, "height": H, "spp": SPP, "integrator": cfg["integrator"],
                        "max_depth": cfg["max_depth"], "global_batch": W * H * SPP,
-                       "parallelism": f"pixel rows y%{world} per GPU + RCCL reduce" if world > 1 else "1 GPU",
+                       "parallelism": (f"pixel rows y%{world} per GPU + RCCL {args.assembly} to rank 0" if world > 1
+                                       else "1 GPU"),
                        "segments_per_sample": round(agg["segments"] / max(1, agg["samples"]), 4),
                        "draws_per_sample": round(agg["draws"] / max(1, agg["samples"]), 4),
                        "iterations_per_frame": round(agg["iterations"] / args.steps, 1),
@@ -373,9 +403,10 @@ def main():
             "roofline": roof,
             "cpu_baseline": None,
         }
-        if world > 1:   # the RCCL framebuffer reduce, inside ms_per_step (slowest rank)
-            out["config"]["reduce_ms_per_step"] = round(reduce_s / args.steps * 1e3, 3)
-            out["config"]["reduce_bytes"] = W * H * 3 * 4
+        if world > 1:   # the RCCL frame assembly, inside ms_per_step (slowest rank)
+            out["config"]["assembly"] = args.assembly
+            out["config"]["assembly_ms_per_step"] = round(reduce_s / args.steps * 1e3, 3)
+            out["config"]["assembly_bytes"] = distributed.assembly_bytes(H, W, world, args.assembly)
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(args.config, cfg, args.cpu_spp)
         print(json.dumps(out), flush=True)

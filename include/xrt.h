@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define XRT_ABI_VERSION 11
+#define XRT_ABI_VERSION 12
 
 /* ---- status codes ---------------------------------------------------------------- */
 enum {
@@ -48,7 +48,10 @@ enum {
 
 /* ---- scene description (flattened Scene) ------------------------------------------ */
 enum { XRT_OBJ_MESH = 0, XRT_OBJ_SPHERE = 1, XRT_OBJ_BOX = 2 };
-enum { XRT_LIGHT_QUAD = 0, XRT_LIGHT_TRIANGLE = 1, XRT_LIGHT_SPHERE = 2 };
+/* XRT_LIGHT_SPHERE: SphereLight::sample's default (cone) branch (Src/light.h:157-197);
+ * XRT_LIGHT_SPHERE_AREA: the same light built with AREA_SAMPLING (Src/light.h:131-135,185-191:
+ * a uniform point on the sphere, UniformSampleSphere Src/light.cpp:99-105, pdf 2 tmax^3/|d.n|) */
+enum { XRT_LIGHT_QUAD = 0, XRT_LIGHT_TRIANGLE = 1, XRT_LIGHT_SPHERE = 2, XRT_LIGHT_SPHERE_AREA = 3 };
 enum { XRT_MAT_NONE = 0, XRT_MAT_LAMBERT = 1 };
 
 /* One Object (Src/primitive.h:40-95) in Scene::m_objects iteration order. */
@@ -201,6 +204,14 @@ typedef struct {
     uint64_t layout_launches[5]; /* merged schedules: step launches per slots-per-wave layout
                                     64, 32, 16, 8, 4 (the layout is re-chosen every launch
                                     from the live count)                                   */
+    /* pixel-parallel chains (XRT_SCHED_PIXEL): which of k_pixel's paths ran */
+    uint64_t pix_windows;        /* candidate windows evaluated (64 offsets each)           */
+    uint64_t pix_stride4;        /* ... of them at stride 4 (after a window of surface hits) */
+    uint64_t pix_frustum;        /* pixels whose camera rays tested a camera-frustum list   */
+    uint64_t pix_frustum_overflow; /* pixels whose frustum list overflowed (BVH walks)      */
+    uint64_t pix_shadow_list;    /* pixels whose shadow rays tested an occluder list        */
+    uint64_t pix_shadow_overflow;  /* pixels whose occluder list overflowed (BVH walks)     */
+    uint64_t pix_flushes;        /* deferred-shading queue flushes                          */
 } xrt_stats;
 
 /* ---- context ----------------------------------------------------------------------- */
@@ -306,6 +317,9 @@ int xrt_hscene_add_triangle_light(xrt_hscene* s, const char* name, const float v
                                   const float v1[3], const float v2[3], const float Le[3]);
 int xrt_hscene_add_sphere_light(xrt_hscene* s, const char* name, const float center[3], float radius,
                                 const float Le[3]);
+/* the same SphereLight as the reference compiled with AREA_SAMPLING (XRT_LIGHT_SPHERE_AREA) */
+int xrt_hscene_add_sphere_light_area(xrt_hscene* s, const char* name, const float center[3], float radius,
+                                     const float Le[3]);
 /* Scene::addObj(name, medium->makeObject()): a BoxMesh over the medium's bounds */
 int xrt_hscene_add_medium_box(xrt_hscene* s, const char* name, const float pmin[3], const float pmax[3]);
 /* Flatten in unordered_map iteration order.  Pointers stay valid until the next

@@ -51,12 +51,20 @@ private:
 
 class SphereLight : public AreaLight {
 public:
-    SphereLight(const Vec3f& center, float radius, const Matrix44f& l2w, const Vec3f& Le);
+    // The reference picks SphereLight::sample's branch at compile time (Src/light.h:131-197):
+    // the default cone sampling, or a uniform point on the sphere with AREA_SAMPLING (off in
+    // its build, Src/cmakelists.txt:63).  Here the choice is per light: Sampling::Area renders
+    // exactly what a reference built with -DAREA_SAMPLING renders.
+    enum class Sampling { Cone, Area };
+    SphereLight(const Vec3f& center, float radius, const Matrix44f& l2w, const Vec3f& Le,
+                Sampling sampling = Sampling::Cone);
     std::unique_ptr<Object> makeObject() override;
     const Vec3f& center() const { return center_; }
     float radius() const { return radius_; }
+    Sampling sampling() const { return sampling_; }
 
 private:
     Vec3f center_;
     float radius_;
+    Sampling sampling_;
 };

@@ -351,6 +351,25 @@ static v3 light_sample(const xrt_light* l, v3 position, v3* wi, float* pdf, floa
         *wi = vdivs(d, *tmax);
         *pdf = (2.f * *tmax * *tmax * *tmax) / fabsf(dn);
         return ld3(l->Le);
+    } else if (l->kind == XRT_LIGHT_SPHERE_AREA) {
+        /* SphereLight::sample with AREA_SAMPLING (Src/light.h:131-135,185-191) and
+         * UniformSampleSphere (Src/light.cpp:99-105).  GCC evaluates the call's second
+         * getNext1D() operand first: the first draw is r2 (phi), the second r1 (z). */
+        v3 center = ld3(l->center);
+        float r2 = orc_draw(rng);
+        float r1 = orc_draw(rng);
+        float z = 1.f - 2.f * r1;
+        float sin_theta = sqrtf(1 - z * z);
+        float phi = PI_MUL_2 * r2;
+        v3 n = mk(cosf(phi) * sin_theta, sinf(phi) * sin_theta, z);
+        v3 p = vadd(center, vmuls(n, l->radius));
+        v3 d = vsub(p, position);
+        *tmax = vlength(d);
+        float dn = vdot(d, n);
+        if (dn >= 0) return mk(0, 0, 0);
+        *wi = vdivs(d, *tmax);
+        *pdf = (2.f * *tmax * *tmax * *tmax) / fabsf(dn);
+        return ld3(l->Le);
     } else {
         /* SphereLight::sample, default (cone) branch (Src/light.h:157-197) */
         v3 center = ld3(l->center);

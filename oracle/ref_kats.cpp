@@ -399,6 +399,57 @@ int main() {
         o.key("frame_l2w"); o.arr(l2w);
     }
 
+    // 11. SphereLight::sample built with AREA_SAMPLING (Src/light.h:131-135,185-191) and its
+    //     UniformSampleSphere (Src/light.cpp:99-105): light.h includes spdlog and is not
+    //     buildable here, so the sampling expression is repeated with the reference's own
+    //     Vec3f, length/dot and UniformSampler — and, to pin GCC's draw order, the call keeps
+    //     its shape: a const member taking (const float& r1, const float& r2), called with two
+    //     getNext1D() operands.
+    {
+        struct AreaProbe {
+            Vec3f center;
+            float radius;
+            Vec3f dirOnSphere(const float& r1, const float& r2) const {
+                float z = 1.f - 2.f * r1;
+                float sin_theta = std::sqrt(1 - z * z);
+                float phi = 2 * PI * r2;
+                return {std::cos(phi) * sin_theta, std::sin(phi) * sin_theta, z};
+            }
+            Vec3f sample(const Vec3f& position, Vec3f& wi, float& pdf, float& tmax, Sampler& s) const {
+                Vec3f n = dirOnSphere(s.getNext1D(), s.getNext1D());
+                Vec3f p = center + n * radius;
+                Vec3f d = p - position;
+                tmax = length(d);
+                float d_dot_n = dot(d, n);
+                if (d_dot_n >= 0) return Vec3f(0.0f);
+                wi = d / tmax;
+                pdf = (2.f * tmax * tmax * tmax) / std::abs(d_dot_n);
+                return Vec3f(1.0f);
+            }
+        };
+        Gen g(0xA2EAu);
+        UniformSampler smp;
+        smp.setSeed(31337);
+        std::vector<uint32_t> in, out;
+        for (int k = 0; k < 512; ++k) {
+            AreaProbe L{g.vec(-20.0f, 20.0f), g.uni(0.2f, 6.0f)};
+            Vec3f pos = g.vec(-30.0f, 30.0f);
+            push3(in, L.center);
+            in.push_back(bits(L.radius));
+            push3(in, pos);
+            Vec3f wi(0.0f);
+            float pdf = 0.0f, tmax = 0.0f;
+            Vec3f le = L.sample(pos, wi, pdf, tmax, smp);
+            push3(out, wi);
+            out.push_back(bits(pdf));
+            out.push_back(bits(tmax));
+            out.push_back(le[0] != 0.0f ? 1u : 0u);
+        }
+        o.key("sphere_area_seed"); o.arr({31337u});
+        o.key("sphere_area_in"); o.arr(in);
+        o.key("sphere_area_out"); o.arr(out);
+    }
+
     o.s += "\n}\n";
     std::fputs(o.s.c_str(), stdout);
     return 0;

@@ -1,5 +1,5 @@
 """CPU stand-in for HipRenderer in bench.py's multi-rank plumbing test (tests/test_bench_launch.py),
-selected with XRT_BENCH_STANDIN=bench_standin:make.  Not the oracle and not a renderer: it
+selected with bench.py --test-standin bench_standin:make.  Not the oracle and not a renderer: it
 writes a known value into the rows a shard owns (zeros elsewhere), so the reduced frame can be
 checked, and returns counters shaped like xrt_stats.  XRT_BENCH_STANDIN_FAIL_RANK=r makes
 rank r raise in its render, to test that a failing rank fails the job."""

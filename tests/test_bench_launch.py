@@ -56,7 +56,6 @@ def _standin_env(tmp_path, **extra):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
                                                              "MASTER_PORT")}
     env["HIP_VISIBLE_DEVICES"] = ""
-    env["XRT_BENCH_STANDIN"] = "bench_standin:make"
     env["XRT_BENCH_STANDIN_DEVICES"] = "2"
     env["XRT_BENCH_STANDIN_OUT"] = str(tmp_path / "frames")
     env["XRT_DIST_TIMEOUT_S"] = "60"
@@ -70,16 +69,18 @@ def test_bench_spawns_two_ranks_end_to_end(tmp_path):
     spawn_ranks' torch.distributed.run child, the rank environment, process-group init (gloo
     with the stand-in renderer; nccl = RCCL on the GPU node), ShardedRenderer's row shards and
     framebuffer reduce, the max-over-ranks timing and the whole-job counters: rank 0 prints
-    exactly one n_gpus 2 line carrying reduce_ms_per_step, and both ranks rendered every step."""
+    exactly one n_gpus 2 line carrying assembly_ms_per_step, and both ranks rendered every step."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--no-cpu", "--config", "C1",
-                        "--steps", "3", "--warmup", "1", "--no-timing"],
+                        "--steps", "3", "--warmup", "1", "--no-timing", "--test-standin", "bench_standin:make"],
                        capture_output=True, text=True, env=_standin_env(tmp_path), timeout=300)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = lines[0]
     assert d["n_gpus"] == 2 and d["steps"] == 3 and "STAND-IN" in d["data"]
-    assert d["config"]["reduce_ms_per_step"] >= 0 and d["config"]["reduce_bytes"] == 256 * 256 * 3 * 4
+    assert d["config"]["assembly"] == "gather" and d["config"]["assembly_ms_per_step"] >= 0
+    assert d["config"]["assembly_bytes"] == 128 * 256 * 3 * 4   # rank 1's 128 packed rows
+    assert "--test-standin" in r.stderr
     assert d["config"]["parallelism"].startswith("pixel rows y%2")
     assert d["config"]["segments_per_sample"] == 1.0 and d["config"]["draws_per_sample"] == 2.0   # summed over ranks
     assert d["value"] > 0 and d["ms_per_step"] > 0
@@ -92,7 +93,7 @@ def test_bench_spawns_two_ranks_end_to_end(tmp_path):
 def test_bench_failing_rank_fails_the_job(tmp_path):
     """A rank that raises ends the job with a non-zero status and no bench line."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--no-cpu", "--config", "C1",
-                        "--steps", "2", "--warmup", "0", "--no-timing"],
+                        "--steps", "2", "--warmup", "0", "--no-timing", "--test-standin", "bench_standin:make"],
                        capture_output=True, text=True, env=_standin_env(tmp_path, XRT_BENCH_STANDIN_FAIL_RANK="1"),
                        timeout=300)
     assert r.returncode != 0

@@ -80,7 +80,7 @@ class _OracleShardRenderer:
         return {"samples": width * len(range(shard_index, height, shard_count)) * self.spp}
 
 
-def _sharded_worker(rank, world, port, out_path, steps):
+def _sharded_worker(rank, world, port, out_path, steps, assembly="gather", dst=0):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
@@ -91,31 +91,39 @@ def _sharded_worker(rank, world, port, out_path, steps):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     s = scenes.cornell(W, H)
     r = _OracleShardRenderer(SPP)
-    sr = distributed.ShardedRenderer(r, dist)
+    sr = distributed.ShardedRenderer(r, dist, dst=dst, assembly=assembly)
     assert sr.rows(H) == distributed.shard_rows(H, rank, world)
     fb = torch.full((H, W, 3), 7.0)   # stale contents: every step overwrites the whole buffer
     frames = []
     for _ in range(steps):
         st = sr.render(s, W, H, fb)
-        if rank == 0:
+        if rank == dst:
             frames.append(fb.numpy().copy())
+        elif assembly == "gather":   # a sender's own buffer is untouched: its rows, zeros elsewhere
+            mine = np.zeros(H, bool)
+            mine[rank::world] = True
+            assert np.all(fb.numpy()[~mine] == 0) and np.any(fb.numpy()[mine] != 0)
     assert r.calls == [(rank, world, None)] * steps
     tot = distributed.sum_counters({"samples": st["samples"], "iterations": 5}, dist)
     assert tot["samples"] == W * H * SPP and tot["iterations"] == 5
-    if rank == 0:
+    if rank == dst:
         np.save(out_path, np.stack(frames))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_renderer_every_step_exact(tmp_path, world):
+@pytest.mark.parametrize("world,assembly,dst", [(2, "gather", 0), (3, "gather", 0), (3, "gather", 1),
+                                                (2, "reduce", 0), (3, "reduce", 0)])
+def test_sharded_renderer_every_step_exact(tmp_path, world, assembly, dst):
     """ShardedRenderer (bench.py's step): several frames in a row into the same buffer, each
-    assembled on rank 0 equal to the one-process render; world 3 leaves uneven row counts."""
+    assembled on rank `dst` equal to the one-process render, by the owned-rows gather (the
+    default: each rank sends only rows y % world == rank, packed) and by the SUM reduce of full
+    framebuffers; world 3 leaves uneven row counts (H = 23: 8, 8, 7 rows, so one packed buffer
+    carries a padding row)."""
     import pyoracle
     from xraytracer_amd import scenes
     out = str(tmp_path / "frames.npy")
-    mp.spawn(_sharded_worker, args=(world, _free_port(), out, 3), nprocs=world, join=True)
+    mp.spawn(_sharded_worker, args=(world, _free_port(), out, 3, assembly, dst), nprocs=world, join=True)
     got = np.load(out)
     full, _ = pyoracle.render(scenes.cornell(W, H), W, H, SPP, nthreads=1)
     assert got.shape[0] == 3
@@ -134,3 +142,14 @@ def test_sharded_renderer_rejects_bad_buffer():
     # row shards + SUM reduce cannot accumulate in place
     with pytest.raises(ValueError):
         sr.render(None, W, H, torch.zeros((H, W, 3)), accumulate=True)
+    with pytest.raises(ValueError):
+        distributed.ShardedRenderer(_OracleShardRenderer(1), None, assembly="allreduce")
+
+
+def test_assembly_bytes():
+    from xraytracer_amd import distributed
+    # C3 1280x720 at 8 ranks: 7 packed 90-row shards vs 7 full 11 MB framebuffers
+    assert distributed.assembly_bytes(720, 1280, 8) == 7 * 90 * 1280 * 12
+    assert distributed.assembly_bytes(720, 1280, 8, "reduce") == 7 * 720 * 1280 * 12
+    assert distributed.assembly_bytes(23, 40, 3) == 2 * 8 * 40 * 12
+    assert distributed.assembly_bytes(600, 800, 1) == 0

@@ -206,4 +206,4 @@ def test_bench_runs_ranks_over_rccl(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     d = json.loads(line)
-    assert d["n_gpus"] == 2 and d["config"]["reduce_ms_per_step"] >= 0.0
+    assert d["n_gpus"] == 2 and d["config"]["assembly_ms_per_step"] >= 0.0 and d["config"]["assembly"] == "gather"

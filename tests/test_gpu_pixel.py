@@ -104,6 +104,11 @@ def test_frustum_lists_and_their_overflow(renderer, wh):
     img, ref, st, g = render_pixel(renderer, s, w, h, 150)
     compare(img, ref)
     counters_equal(g, st)
+    # which of k_pixel's paths ran (xrt_stats pix_*): every pixel builds a list or overflows
+    assert g.pix_frustum + g.pix_frustum_overflow == w * h
+    assert g.pix_frustum_overflow > 0
+    if wh == (23, 13):
+        assert g.pix_frustum > 0
 
 
 def far_cluster(w, h, n=300, seed=11):
@@ -135,6 +140,7 @@ def test_block_culled_lists_far_from_origin(renderer, wh):
     compare(img, ref)
     counters_equal(g, st)
     assert st["shadow_rays"] > 0
+    assert g.pix_frustum > 0 and g.pix_shadow_list > 0 and g.pix_flushes > 0
 
 
 @pytest.mark.parametrize("spp", [1, 2, 21, 31, 32, 33, 63, 64, 65, 127, 129, 300])
@@ -234,6 +240,39 @@ def test_shadow_occluder_lists(renderer, light):
         img, ref, st, g = render_pixel(renderer, s, w, h, 70, integrator="direct")
         compare(img, ref)
         counters_equal(g, st)
+        if (w, h) == (48, 27):
+            assert g.pix_shadow_list > 0
+
+
+def covered_block(w, h):
+    """A big sphere filling the whole view (every camera ray of every pixel hits it), a
+    sphere light beside the camera and a few small occluders between them: every window of
+    every pixel is all surface hits, so after each pixel's first window the chain runs in
+    stride-4 windows (pixel.hip) with one-sphere frustum lists and shadow-occluder lists."""
+    s = scenes.SceneBundle()
+    s.add_sphere("big", (0.0, 0.0, -12.0), 6.0, (0.6, 0.5, 0.4))
+    for k in range(6):
+        s.add_sphere(f"occ{k}", (2.0 + 0.7 * k, 3.0 + 0.3 * k, -4.0 - 0.5 * k), 0.35, (0.5, 0.5, 0.5))
+    s.add_sphere_light("SphereLight", (6.0, 6.0, -2.0), 1.0, (25.0, 25.0, 25.0))
+    s.flatten()
+    s.camera = scenes.pinhole((1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1), 20.0, w, h)
+    s.integrator, s.max_depth = "direct", 1
+    return s
+
+
+def test_stride4_windows_on_a_covered_block(renderer):
+    """Stride-4 windows forced: 512 spp on pixels whose every sample hits a surface.  Per
+    pixel: one stride-2 window (32 samples), then 7 stride-4 windows of 64 samples each while
+    at least 64 samples remain, then the last 32 at stride 2.  Bit-exact, counters equal."""
+    w, h = 16, 12
+    s = covered_block(w, h)
+    img, ref, st, g = render_pixel(renderer, s, w, h, 512)
+    compare(img, ref)
+    counters_equal(g, st)
+    assert st["draws"] == w * h * 512 * 4   # every sample: 2 jitter + 2 light words
+    assert g.pix_stride4 == 7 * w * h and g.pix_windows == 9 * w * h
+    assert g.pix_frustum == w * h and g.pix_shadow_list == w * h and g.pix_flushes > 0
+    assert st["shadow_rays"] > 0 and img.mean() > 0
 
 
 def test_shards_and_step_schedule_agree(renderer):
@@ -281,6 +320,22 @@ def test_c3_headline_geometry(renderer):
     k, n = 21, 64
     ref, st = pyoracle.render(scene, 1280, 720, 96, shard_index=k, shard_count=n)
     compare(img[k::n], ref[k::n])
+
+
+def test_c3_fast_paths_in_compared_rows(renderer):
+    """C3 at 1280x720, 96 spp, rendered as the row shard y % 64 == 29 (rows 29 ... 669, most
+    of them >= 405, where the sphere field fills the pixels), so the counters describe exactly
+    the compared rows: frustum lists, shadow-occluder lists, deferred flushes and stride-4
+    windows all ran there, and the rows are bit-exact."""
+    scene, img, g = render_c3(renderer, 96, shard_index=29, shard_count=64)
+    assert g.schedule == abi.XRT_SCHED_PIXEL
+    npx = 11 * 1280
+    assert g.samples == npx * 96
+    assert g.pix_frustum > 0 and g.pix_shadow_list > 0 and g.pix_flushes > 0 and g.pix_stride4 > 0
+    assert g.pix_frustum + g.pix_frustum_overflow == npx
+    ref, st = pyoracle.render(scene, 1280, 720, 96, shard_index=29, shard_count=64)
+    compare(img[29::64], ref[29::64])
+    assert (g.shadow_rays, g.draws) == (st["shadow_rays"], st["draws"])
 
 
 def test_c3_row_shard(renderer):

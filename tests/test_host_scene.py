@@ -149,3 +149,16 @@ def test_tinyobj_ear_clipping_polygons(tmp_path, name, pts):
     assert abs(sum(areas) - poly2) < 1e-3
     verts = {tuple(np.float32(v)) for v in np.array([(x, y, 1.0) for x, y in pts], np.float32)}
     assert all(tuple(v) in verts for t in tris for v in t)
+
+
+def test_sphere_light_sampling_kind_in_flattened_scene():
+    """SphereLight::Sampling::Area (the reference's AREA_SAMPLING build, Src/light.h:131-135)
+    flattens to XRT_LIGHT_SPHERE_AREA, the default to the cone-sampled XRT_LIGHT_SPHERE."""
+    from xraytracer_amd import abi, scenes
+    for area, kind in ((True, abi.XRT_LIGHT_SPHERE_AREA), (False, abi.XRT_LIGHT_SPHERE)):
+        s = scenes.SceneBundle()
+        s.add_sphere("ball", (0.0, 0.0, -3.0), 0.5, (0.5, 0.5, 0.5))
+        s.add_sphere_light("SphereLight", (0.0, 4.0, -3.0), 1.0, (10.0, 10.0, 10.0), area=area)
+        s.flatten()
+        assert s.desc.n_lights == 1 and s.desc.lights[0].kind == kind
+        assert [s.desc.lights[0].center[q] for q in range(3)] == [0.0, 4.0, -3.0]

@@ -223,3 +223,34 @@ def test_lambert_bxdf_through_material_interface(golden):
         assert np.array_equal(bits(f), f_ref[k]), k
         assert np.array_equal(bits(wi), wi_ref[k]), k
         assert bits(pdf)[0] == pdf_ref[k]
+
+
+def test_sphere_light_area_sampling(golden):
+    """SphereLight::sample built with AREA_SAMPLING (Src/light.h:131-135,185-191) and
+    UniformSampleSphere (Src/light.cpp:99-105), evaluated by the reference's own Vec3f /
+    UniformSampler code with the call's shape kept (GCC: the first draw is r2): wi, pdf,
+    tmax and whether the sample faces the point, for 512 lights and points on one stream."""
+    from xraytracer_amd import abi
+    lib = pyoracle.lib()
+    m = pyoracle.mt(golden["sphere_area_seed"][0])
+    inp = f32(golden["sphere_area_in"]).reshape(-1, 7)
+    ref = np.asarray(golden["sphere_area_out"], np.uint32).reshape(-1, 6)
+    front = 0
+    for k in range(len(inp)):
+        lt = abi.XrtLight()
+        lt.kind = abi.XRT_LIGHT_SPHERE_AREA
+        for q in range(3):
+            lt.center[q] = float(inp[k, q])
+            lt.Le[q] = 1.0
+        lt.radius = float(inp[k, 3])
+        pos = np.ascontiguousarray(inp[k, 4:7])
+        out = np.zeros(8, np.float32)
+        lib.orc_kat_light(C.byref(m), C.byref(lt), pyoracle.fp(pos), pyoracle.fp(out))
+        faces = int(ref[k, 5])
+        front += faces
+        assert int(out[5] != 0.0) == faces, k
+        assert bits(out[4:5])[0] == ref[k, 4], k          # tmax is written either way
+        if faces:
+            assert np.array_equal(bits(out[0:3]), ref[k, 0:3]), k
+            assert bits(out[3:4])[0] == ref[k, 3], k
+    assert 100 < front < 412   # both outcomes are covered

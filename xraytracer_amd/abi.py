@@ -17,10 +17,10 @@ if os.environ.get("XRT_LIB"):   # experiment builds (csrc/Makefile `variant` -> 
     _v = os.path.join(HERE, "variants", os.environ["XRT_LIB"])
     LIB_PATH = _v if os.path.exists(_v) else os.path.join(HERE, os.environ["XRT_LIB"])
 
-XRT_ABI_VERSION = 11  # include/xrt.h XRT_ABI_VERSION
+XRT_ABI_VERSION = 12  # include/xrt.h XRT_ABI_VERSION
 XRT_OK = 0
 XRT_OBJ_MESH, XRT_OBJ_SPHERE, XRT_OBJ_BOX = 0, 1, 2
-XRT_LIGHT_QUAD, XRT_LIGHT_TRIANGLE, XRT_LIGHT_SPHERE = 0, 1, 2
+XRT_LIGHT_QUAD, XRT_LIGHT_TRIANGLE, XRT_LIGHT_SPHERE, XRT_LIGHT_SPHERE_AREA = 0, 1, 2, 3
 XRT_MAT_NONE, XRT_MAT_LAMBERT = 0, 1
 XRT_INTEGRATOR_GI, XRT_INTEGRATOR_DIRECT, XRT_INTEGRATOR_VPT = 0, 1, 2
 XRT_INTEGRATOR_INDIRECT, XRT_INTEGRATOR_NORMAL, XRT_INTEGRATOR_VPT_NEE = 3, 4, 5
@@ -93,7 +93,10 @@ class XrtStats(C.Structure):
                 ("rejected", C.c_uint64), ("iterations", C.c_uint64), ("path_slots", C.c_uint64),
                 ("schedule", C.c_uint64), ("stalled", C.c_uint64), ("slots_per_wave", C.c_uint32),
                 ("group_lanes", C.c_uint32), ("partitions", C.c_uint32), ("visits_per_launch", C.c_uint32),
-                ("rng_twists", C.c_uint64), ("layout_launches", C.c_uint64 * 5)]
+                ("rng_twists", C.c_uint64), ("layout_launches", C.c_uint64 * 5),
+                ("pix_windows", C.c_uint64), ("pix_stride4", C.c_uint64), ("pix_frustum", C.c_uint64),
+                ("pix_frustum_overflow", C.c_uint64), ("pix_shadow_list", C.c_uint64),
+                ("pix_shadow_overflow", C.c_uint64), ("pix_flushes", C.c_uint64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kernel_ms", "launches", "layout_launches")}
@@ -138,6 +141,7 @@ SIGNATURES = {
     "xrt_hscene_add_quad_light": (C.c_int, [C.c_void_p, C.c_char_p, f32p, f32p, f32p, f32p]),
     "xrt_hscene_add_triangle_light": (C.c_int, [C.c_void_p, C.c_char_p, f32p, f32p, f32p, f32p]),
     "xrt_hscene_add_sphere_light": (C.c_int, [C.c_void_p, C.c_char_p, f32p, C.c_float, f32p]),
+    "xrt_hscene_add_sphere_light_area": (C.c_int, [C.c_void_p, C.c_char_p, f32p, C.c_float, f32p]),
     "xrt_hscene_add_medium_box": (C.c_int, [C.c_void_p, C.c_char_p, f32p, f32p]),
     "xrt_hscene_flatten": (C.c_int, [C.c_void_p, C.POINTER(XrtSceneDesc)]),
     "xrt_hscene_object_name": (C.c_char_p, [C.c_void_p, C.c_uint32]),

@@ -121,6 +121,14 @@ int xrt_hscene_add_sphere_light(xrt_hscene* s, const char* name, const float cen
     return XRT_OK;
 }
 
+int xrt_hscene_add_sphere_light_area(xrt_hscene* s, const char* name, const float center[3], float radius,
+                                     const float Le[3]) {
+    if (!s || !name || !center || !Le) return XRT_ERR_INVALID;
+    s->scene.addAreaLight(name, std::make_unique<SphereLight>(v3(center), radius, Matrix44f(), v3(Le),
+                                                              SphereLight::Sampling::Area));
+    return XRT_OK;
+}
+
 int xrt_hscene_add_medium_box(xrt_hscene* s, const char* name, const float pmin[3], const float pmax[3]) {
     if (!s || !name || !pmin || !pmax) return XRT_ERR_INVALID;
     if (s->media.empty()) s->media.push_back(std::make_unique<FacadeMedium>());

@@ -93,8 +93,8 @@ std::unique_ptr<Object> TriangleLight::makeObject() {  // Src/light.cpp:35-41
     return std::make_unique<Mesh>(std::move(prims), nullptr, this);
 }
 
-SphereLight::SphereLight(const Vec3f& center, float radius, const Matrix44f& l2w, const Vec3f& Le)
-    : AreaLight(Kind::Sphere, l2w, Le), center_(multVecMatrix(center, l2w)), radius_(radius) {}
+SphereLight::SphereLight(const Vec3f& center, float radius, const Matrix44f& l2w, const Vec3f& Le, Sampling sampling)
+    : AreaLight(Kind::Sphere, l2w, Le), center_(multVecMatrix(center, l2w)), radius_(radius), sampling_(sampling) {}
 
 std::unique_ptr<Object> SphereLight::makeObject() {  // Src/light.cpp:93-97
     return std::make_unique<Sphere>(center_, radius_, nullptr, this);
@@ -770,7 +770,7 @@ int Scene::flatten(xrt_scene_desc* out) const {
             d.kind = XRT_LIGHT_TRIANGLE;
             put3(d.v0, t->v0()), put3(d.v1, t->v1()), put3(d.v2, t->v2());
         } else if (auto* s = dynamic_cast<const SphereLight*>(l.get())) {
-            d.kind = XRT_LIGHT_SPHERE;
+            d.kind = s->sampling() == SphereLight::Sampling::Area ? XRT_LIGHT_SPHERE_AREA : XRT_LIGHT_SPHERE;
             put3(d.center, s->center());
             d.radius = s->radius();
         } else {

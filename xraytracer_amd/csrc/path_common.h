@@ -489,7 +489,8 @@ __device__ __forceinline__ v3 ld3(const float* p) { return mk(p[0], p[1], p[2]);
 
 // QuadLight::sample (Src/light.cpp:59-68; first draw scales e2 under GCC),
 // TriangleLight::sample (light.cpp:21-30,43-47; first draw is v),
-// SphereLight::sample default branch (light.h:157-197).  pdf is left untouched on the
+// SphereLight::sample default branch (light.h:157-197) or, kind 3, its AREA_SAMPLING
+// branch (light.h:131-135,185-191).  pdf is left untouched on the
 // back-facing early return, as in the reference.
 template <class RNG>
 __device__ inline v3 light_sample(const DLight& L, v3 x, v3& wi, float& pdf, float& tmax, RNG& rng) {
@@ -512,6 +513,24 @@ __device__ inline v3 light_sample(const DLight& L, v3 x, v3& wi, float& pdf, flo
         const v3 dd = p - x;
         tmax = length(dd);
         const float dn = dot(dd, ld3(L.Ng));
+        if (dn >= 0.0f) return mk(0, 0, 0);
+        wi = dd / tmax;
+        pdf = (2.0f * tmax * tmax * tmax) / __builtin_fabsf(dn);
+        return ld3(L.Le);
+    } else if (L.kind == 3) {
+        // SphereLight::sample built with AREA_SAMPLING (Src/light.h:131-135,185-191):
+        // UniformSampleSphere(r1, r2) (Src/light.cpp:99-105) with GCC's right-to-left
+        // operands — the first draw is r2 (phi), the second r1 (z)
+        const float r2 = rng.next();
+        const float r1 = rng.next();
+        const float z = 1.f - 2.f * r1;
+        const float sin_theta = __builtin_sqrtf(1.0f - z * z);
+        float sphi, cphi;
+        glibc_sincosf(kPI_MUL_2 * r2, sphi, cphi);
+        const v3 nn = mk(cphi * sin_theta, sphi * sin_theta, z);
+        const v3 dd = (ld3(L.center) + nn * L.radius) - x;
+        tmax = length(dd);
+        const float dn = dot(dd, nn);
         if (dn >= 0.0f) return mk(0, 0, 0);
         wi = dd / tmax;
         pdf = (2.0f * tmax * tmax * tmax) / __builtin_fabsf(dn);

@@ -209,12 +209,12 @@ __device__ int pix_shadow_list(const KParams& P, const LScene& L, f4 lsph, int n
     const DLight& lt = L.light[0];
     v3 lc;
     float lr;
-    if (lt.kind == 2) {
+    if (lt.kind == XRT_LIGHT_SPHERE || lt.kind == XRT_LIGHT_SPHERE_AREA) {   // either sampling: a point on the sphere
         lc = ld3(lt.center), lr = __builtin_fabsf(lt.radius);
     } else {   // quad / triangle: the centroid of its corners and the farthest corner
         const v3 v0 = ld3(lt.v0), e1 = ld3(lt.e1), e2 = ld3(lt.e2);
         const v3 cs[4] = {v0, v0 + e1, v0 + e2, v0 + e1 + e2};
-        const int nc = lt.kind == 0 ? 4 : 3;
+        const int nc = lt.kind == XRT_LIGHT_QUAD ? 4 : 3;
         lc = mk(0, 0, 0);
         for (int q = 0; q < nc; ++q) lc = lc + cs[q];
         lc = lc / (float)nc;
@@ -298,6 +298,10 @@ constexpr bool pix_defer(int scn, int integ) {
     return XRT_PIX_DEFER && scn == SCN_SPHERE && integ == XRT_INTEGRATOR_DIRECT;
 }
 constexpr uint32_t kPixPend = 192;   // pending samples of three windows (codes)
+// the 624-word stream buffer holds three windows' items and the generation lookahead only for
+// NL <= 18 (above), and the plain window's own words bound NL further; xrt_api.cpp refuses
+// scenes with more than kMaxLights lights
+static_assert(kMaxLights <= 18, "k_pixel's stream window assumes at most 18 area lights");
 constexpr uint32_t kPixWaveDeferLds = kPixWaveLds + 3 * kPixSumStride * 4 + 3 * 64 * 4 + kPixPend;
 constexpr int pix_block(int scn, int integ) { return pix_defer(scn, integ) ? XRT_PIX_DEFER_BLOCK : kPixBlock; }
 __host__ __device__ inline bool pix_defer_rt(const KParams& P) {
@@ -334,6 +338,9 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
     // words a surface hit draws beyond its jitter, in pairs: one pair per area light (Direct)
     const uint32_t NLD = INTEG == XRT_INTEGRATOR_DIRECT ? (uint32_t)P.n_lights : 0u;
     const uint32_t per_window = (64u + NLD) / (1u + NLD);   // most surface hits one window's chain holds
+    // which paths ran (xrt_stats pix_*), per wave, added to KParams::stats when the wave retires:
+    // windows, stride-4 windows, frustum lists, their overflows, shadow lists, their overflows, flushes
+    uint32_t cnt_win = 0, cnt_s4 = 0, cnt_fr = 0, cnt_fro = 0, cnt_sl = 0, cnt_slo = 0, cnt_fl = 0;
     for (;;) {
         uint32_t s = 0;
         if (lane == 0) s = atomicAdd(work, 1u);
@@ -353,6 +360,8 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
             wave_sync();
         }
         const int nlist = frustum ? pix_frustum<SCN>(P, L, col, row, list, lane) : -1;
+        cnt_fr += nlist >= 0 ? 1u : 0u;
+        cnt_fro += frustum && nlist < 0 ? 1u : 0u;
         f4 lsph = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // lane e: list entry e's sphere and index
         int lk = 0;
         if (lane < nlist) {
@@ -367,6 +376,8 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
             wave_sync();   // every lane has read its camera-list entry
             nsl = pix_shadow_list(P, L, lsph, nlist, list, lane);
             if (lane < nsl) ssph = L.ssph[list[lane]];
+            cnt_sl += nsl >= 0 ? 1u : 0u;
+            cnt_slo += nsl < 0 ? 1u : 0u;
         }
         float* px = P.fb + 3 * ((size_t)col + (size_t)P.width * row);
         float acc = lane < 3 ? px[lane] : 0.0f;   // lane c < 3: channel c of the running sum
@@ -467,6 +478,7 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
                 add_in_order(vm, val);
             }
             qn = 0, pn = 0, pw = 0;
+            ++cnt_fl;
         };
 
         while (k < P.spp) {
@@ -480,6 +492,8 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
             const bool s4 = DEFER && NLD == 1 && kPixStride4 && s4next && rem >= 64u;
             if (s4 && qn) flush();
             const uint32_t stride = s4 ? 4u : 2u;
+            ++cnt_win;
+            cnt_s4 += s4 ? 1u : 0u;
             const uint32_t span = rem >= 64u ? 64u : min(64u, rem * (1u + NLD));
             const uint32_t need = o + stride * span + 2u * NLD;   // words this window may read
             while (g < need) {
@@ -606,6 +620,12 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
             P.state[s] = ST_DONE;
         }
     }
+    if (lane == 0) {   // wave-uniform counts: one add per counter and wave
+        const uint32_t c[7] = {cnt_win, cnt_s4, cnt_fr, cnt_fro, cnt_sl, cnt_slo, cnt_fl};
+#pragma unroll
+        for (int q = 0; q < 7; ++q)
+            if (c[q]) atomicAdd(P.stats + kStatsPix + q, (unsigned long long)c[q]);
+    }
 }
 
 }  // namespace xrt
@@ -615,7 +635,10 @@ __global__ __launch_bounds__(BS, XRT_PIX_WAVES) void k_pixel(KParams P, uint32_t
 namespace xrt {
 
 bool use_pixel(const KParams& P) {
-    return one_hit(P.integrator) && step_lds_bytes(P) != 0 && pix_lds_bytes(P) <= kPixLds;
+    // within the design budget and what this device gives a workgroup (an oversize k_pixel
+    // launch would fail; the per-slot schedule serves the scene instead)
+    return one_hit(P.integrator) && step_lds_bytes(P) != 0 && pix_lds_bytes(P) <= kPixLds &&
+           pix_lds_bytes(P) <= P.lds_max;
 }
 
 size_t pix_lds_bytes(const KParams& P) {

@@ -132,6 +132,7 @@ constexpr int kSmallTris = 1024;   // scenes up to this size keep every triangle
 constexpr int kLargeObjTris = 256;  // two-level trace: mesh objects above this go into the BVH
 constexpr int kSmallObjs = 256;
 constexpr unsigned kStepLds = 64u * 1024u;   // LDS budget of the fused schedule (k_step)
+constexpr int kStatsPix = 8;                // KParams::stats words 8..14: k_pixel path counters (xrt_stats pix_*)
 constexpr int kStatsWork = 32;               // KParams::stats word k_pixel counts the pixels taken in
 constexpr unsigned kPixLds = 160u * 1024u;   // k_pixel: scene + per-wave stream windows (gfx950: 160 KiB per workgroup)
 
@@ -223,6 +224,7 @@ struct KParams {
     uint32_t rng_keep;           // fused schedule refill threshold (words ahead)
     uint32_t spw_req;            // merged schedule: requested slots per wave (0 = by live count)
     uint32_t rflags;             // xrt_render_params.flags
+    uint32_t lds_max;            // the device's LDS bytes per workgroup (hipDeviceAttributeMaxSharedMemoryPerBlock)
     // ---- slot state (SoA)
     f4 *ray_o, *ray_d, *thr, *rad, *thr_prev;
     f4 *hit;     // t, u, v, code(bits)        code: -1 miss, (kind << 28) | prim

@@ -228,6 +228,12 @@ int xrt_create(int device, xrt_ctx** out) {
             xrt_destroy(c);
             return XRT_ERR_HIP;
         }
+    int lds = 0;
+    if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess || lds <= 0) {
+        xrt_destroy(c);
+        return XRT_ERR_HIP;
+    }
+    c->base.lds_max = (uint32_t)lds;
     *out = c;
     return XRT_OK;
 }
@@ -356,6 +362,8 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
     std::vector<DLight> lights;
     for (uint32_t l = 0; l < s->n_lights; ++l) {
         const xrt_light& L = s->lights[l];
+        if (L.kind < XRT_LIGHT_QUAD || L.kind > XRT_LIGHT_SPHERE_AREA)
+            return set_err(c, XRT_ERR_INVALID, "light " + std::to_string(l) + ": unknown kind");
         DLight d{};
         d.kind = L.kind;
         const Vec3f v0 = V(L.v0), v1 = V(L.v1), v2 = V(L.v2);
@@ -550,7 +558,7 @@ static int upload_scene_one(xrt_ctx* c, const xrt_scene_desc* s) {
     // Sphere boxes: center +- radius, padded by 1e-4 of the scene diagonal + 1e-4 —
     // far above the float error of Sphere::intersect's hit point (and of its
     // near-tangent discriminant), so a box test never drops a hit the linear scan accepts.
-    P.snode = nullptr, P.ssph = nullptr, P.sbk = nullptr, P.n_snode = 0, P.sph_pad = 0.0f;
+    P.snode = nullptr, P.ssph = nullptr, P.sbk = nullptr, P.sblk = nullptr, P.n_snode = 0, P.sph_pad = 0.0f;
     if (P.scene_kind == SCN_SPHERE && P.n_sph >= kSphBvhMin && !exp_env("XRT_NO_BVH")) {
         const size_t ns = (size_t)P.n_sph;
         std::vector<float> mn(3 * ns), mx(3 * ns);
@@ -1059,6 +1067,9 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
                      " in-wave walks %llu\n", hs[38], hs[39], hs[37], hs[36], hs[35]);
     S.segments = hs[0], S.shadow_rays = hs[1], S.draws = hs[2], S.rejected = hs[3], S.stalled = hs[4];
     S.rng_twists = hs[7];
+    S.pix_windows = hs[kStatsPix], S.pix_stride4 = hs[kStatsPix + 1], S.pix_frustum = hs[kStatsPix + 2];
+    S.pix_frustum_overflow = hs[kStatsPix + 3], S.pix_shadow_list = hs[kStatsPix + 4];
+    S.pix_shadow_overflow = hs[kStatsPix + 5], S.pix_flushes = hs[kStatsPix + 6];
     S.schedule = pixel   ? XRT_SCHED_PIXEL
                  : !fused ? XRT_SCHED_WAVEFRONT
                  : bvh    ? XRT_SCHED_STEP_BVH
@@ -1238,6 +1249,9 @@ static int render_multi(xrt_ctx* m, const xrt_render_params* p, float* d_out, fl
             T.samples += S[i].samples, T.segments += S[i].segments, T.shadow_rays += S[i].shadow_rays;
             T.draws += S[i].draws, T.rejected += S[i].rejected, T.stalled += S[i].stalled;
             T.rng_twists += S[i].rng_twists;
+            T.pix_windows += S[i].pix_windows, T.pix_stride4 += S[i].pix_stride4, T.pix_frustum += S[i].pix_frustum;
+            T.pix_frustum_overflow += S[i].pix_frustum_overflow, T.pix_shadow_list += S[i].pix_shadow_list;
+            T.pix_shadow_overflow += S[i].pix_shadow_overflow, T.pix_flushes += S[i].pix_flushes;
             for (int k = 0; k < 5; ++k) T.layout_launches[k] += S[i].layout_launches[k];
             T.path_slots += S[i].path_slots;
             T.iterations = std::max(T.iterations, S[i].iterations);

@@ -179,9 +179,10 @@ class SceneBundle:
                                                             abi.fptr(abi.f3(v1)), abi.fptr(abi.f3(v2)),
                                                             abi.fptr(abi.f3(Le))), f"TriangleLight({name})")
 
-    def add_sphere_light(self, name, center, radius, Le):
-        self._check(self._lib.xrt_hscene_add_sphere_light(self.h, name.encode(), abi.fptr(abi.f3(center)),
-                                                          C.c_float(radius), abi.fptr(abi.f3(Le))),
+    def add_sphere_light(self, name, center, radius, Le, area=False):
+        """SphereLight; area=True: the reference's AREA_SAMPLING build (Src/light.h:131-135)"""
+        fn = self._lib.xrt_hscene_add_sphere_light_area if area else self._lib.xrt_hscene_add_sphere_light
+        self._check(fn(self.h, name.encode(), abi.fptr(abi.f3(center)), C.c_float(radius), abi.fptr(abi.f3(Le))),
                     f"SphereLight({name})")
 
     def add_medium(self, name, medium: Medium):
