@@ -140,6 +140,9 @@ enum {
                                    depend on either                                            */
     XRT_FLAG_NO_PIXEL = 128u,   /* Direct / Normal: the per-slot fused schedule (k_step) instead
                                    of pixel-parallel sample chains (k_pixel); same results     */
+    XRT_FLAG_SPEC = 256u,       /* GI, one light, small triangle scenes: the merged schedule's
+                                   16-slot launches start every sample speculatively beside its
+                                   predecessor's last trace (k_step_spec); same results        */
     XRT_FLAG_ACCUMULATE = 16u  /* Renderer::render's in-place contract (Src/renderer.cpp:75,98):
                                   each owned pixel starts from the value already in the output
                                   buffer (Image::addPixel adds to it in sample order), then
@@ -212,6 +215,7 @@ typedef struct {
     uint64_t pix_shadow_list;    /* pixels whose shadow rays tested an occluder list        */
     uint64_t pix_shadow_overflow;  /* pixels whose occluder list overflowed (BVH walks)     */
     uint64_t pix_flushes;        /* deferred-shading queue flushes                          */
+    uint64_t spec_launches;      /* merged schedule: step launches with speculative starts  */
 } xrt_stats;
 
 /* ---- context ----------------------------------------------------------------------- */

@@ -71,7 +71,7 @@ def main():
     r = HipRenderer(SPP, device=0)
     r.upload(scene)
     fb = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0")
-    kw = dict(slots_per_wave=spw, group=group, deep=deep, schedule=sched)
+    kw = dict(slots_per_wave=spw, group=group, deep=deep, schedule=sched, spec="--spec" in sys.argv)
     r.render_device(scene, W, H, fb.data_ptr(), shard_index=0, shard_count=1, **kw)   # warm: full-frame buffers
     torch.cuda.synchronize()
     res = {}

@@ -57,7 +57,8 @@ static v3 integrate_gi_ev(const scene_ctx* C, v3 ro, v3 rd, uint32_t max_depth, 
     return radiance;
 }
 
-/* visits[q*2+0]: chain length today (one trace per visit), [q*2+1]: with speculation */
+/* visits[q*3+0]: chain length today (one trace per visit), [q*3+1]: with speculation on a
+ * predicted surface hit, [q*3+2]: with every possible next start enumerated */
 int sim_visits(const xrt_scene_desc* S, const orc_camera* cam, const xrt_render_params* p, const uint32_t* pi,
                const uint32_t* pj, uint32_t n, uint32_t* visits) {
     scene_ctx C;
@@ -67,18 +68,26 @@ int sim_visits(const xrt_scene_desc* S, const orc_camera* cam, const xrt_render_
         orc_mt rng;
         orc_mt_seed(&rng, pj[q] + p->width * pi[q]);
         path_counters pc = {0, 0, 0, 0, 0};
-        uint32_t spec_saved = 0;
+        uint32_t spec_saved = 0, enum_visits = 0, unspec = 1;
         for (uint32_t k = 0; k < p->spp; ++k) {
             const float u = ((float)(int)pj[q] + orc_draw(&rng)) / (float)p->width;
             const float v = ((float)(int)pi[q] + orc_draw(&rng)) / (float)p->height;
             v3 ro, rd;
             camera_ray(cam, u, v, &ro, &rd);
             int lp, lok;
+            const uint64_t seg0 = pc.segments;
             (void)integrate_gi_ev(&C, ro, rd, p->max_depth, &rng, &pc, &lp, &lok);
             if (lok && k + 1 < p->spp) spec_saved++;
+            /* enumerated speculation: every possible next-sample start of a sample's last trace
+             * ({c, c+1, c+5}) traced with it and its bounce 0 shaded in the same visit; a start
+             * after a sample that ended at its camera ray is traced on its own visit */
+            const uint32_t segs = (uint32_t)(pc.segments - seg0);
+            enum_visits += segs - 1 + unspec;
+            unspec = segs == 1;
         }
-        visits[q * 2] = (uint32_t)pc.segments;
-        visits[q * 2 + 1] = (uint32_t)pc.segments - spec_saved;
+        visits[q * 3] = (uint32_t)pc.segments;
+        visits[q * 3 + 1] = (uint32_t)pc.segments - spec_saved;
+        visits[q * 3 + 2] = enum_visits;
     }
     return 0;
 }

@@ -26,11 +26,11 @@ s = scenes.build(cfg_name)
 pix = [(i, j) for i in range(0, H, stride) for j in range(0, W, stride)]
 pi = np.array([q[0] for q in pix], np.uint32)
 pj = np.array([q[1] for q in pix], np.uint32)
-vis = np.zeros((len(pix), 2), np.uint32)
+vis = np.zeros((len(pix), 3), np.uint32)
 p = pyoracle.params(s, W, H, SPP)
 u32p = C.POINTER(C.c_uint32)
 lib.sim_visits(C.byref(s.desc), C.byref(pyoracle.camera(s.camera)), C.byref(p), pi.ctypes.data_as(u32p),
                pj.ctypes.data_as(u32p), len(pix), vis.ctypes.data_as(u32p))
-for k, name in ((0, "today"), (1, "speculative")):
+for k, name in ((0, "today"), (1, "speculative"), (2, "enumerated")):
     v = vis[:, k]
     print(f"{name:12s} mean {v.mean():8.1f}  p99 {np.percentile(v, 99):8.1f}  max {v.max():6d}")

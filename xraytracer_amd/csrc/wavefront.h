@@ -225,6 +225,7 @@ struct KParams {
     uint32_t spw_req;            // merged schedule: requested slots per wave (0 = by live count)
     uint32_t rflags;             // xrt_render_params.flags
     uint32_t lds_max;            // the device's LDS bytes per workgroup (hipDeviceAttributeMaxSharedMemoryPerBlock)
+    uint4* camlist;              // speculative starts (spec.hip): per slot the pixel's camera-ray triangle list
     // ---- slot state (SoA)
     f4 *ray_o, *ray_d, *thr, *rad, *thr_prev;
     f4 *hit;     // t, u, v, code(bits)        code: -1 miss, (kind << 28) | prim

@@ -51,7 +51,7 @@ struct xrt_ctx {
     // slots
     size_t cap_slots = 0;
     DevBuf ray_o, ray_d, thr, rad, thr_prev, hit, hit2, hit3, sh_o, sh_d, sh_c, med, med2, nee;
-    DevBuf state, sample_k, depth, occ, rng_c, rng_g, ring, c_seg, c_shadow, c_rej, c_stall, lists, deep;
+    DevBuf state, sample_k, depth, occ, rng_c, rng_g, ring, c_seg, c_shadow, c_rej, c_stall, lists, deep, camlist;
     DevBuf counts, stats, fb, scratch, kparams;
     size_t cap_fb = 0;
     uint32_t* h_poll = nullptr;  // pinned
@@ -252,7 +252,7 @@ void xrt_destroy(xrt_ctx* c) {
     for (DevBuf* b : all) free_buf(*b);
     free_buf(c->stri), free_buf(c->sbox), free_buf(c->splane), free_buf(c->bvh4), free_buf(c->deep);
     free_buf(c->stage), free_buf(c->q_rays), free_buf(c->q_tmax), free_buf(c->q_out);
-    free_buf(c->brick_table), free_buf(c->brick_data), free_buf(c->corners);
+    free_buf(c->brick_table), free_buf(c->brick_data), free_buf(c->corners), free_buf(c->camlist);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->poll_ev)
         if (e) (void)hipEventDestroy(e);
@@ -843,6 +843,8 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     const bool pixel = !bvh && !(p->flags & (XRT_FLAG_WAVEFRONT | XRT_FLAG_NO_PIXEL)) && use_pixel(P);
     const bool fused = bvh || (!(p->flags & XRT_FLAG_WAVEFRONT) && step_lds_bytes(P) != 0);
     const bool merged = bvh || (fused && !(p->flags & XRT_FLAG_NO_MERGED) && use_step_merged(P));
+    // speculative sample starts for the merged schedule's 16-slot launches (spec.hip)
+    const bool spec = merged && !bvh && (p->flags & XRT_FLAG_SPEC) && use_step_spec(P);
     // live-list partitions (a multiple of the 8 XCDs): every wave appends to its partition's
     // counters once per launch, so more partitions mean less atomic contention (64 -> 256:
     // C4 -14%, C2 -4.5%).  The merged schedule (64 segments per launch) is fastest with
@@ -909,6 +911,11 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
         HIPCHK(c, hipMemcpyAsync(fb, h_out, npix * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(P.stats, 0, 512, c->stream));
     HIPCHK(c, launch(XRT_K_SEED, [&] { return launch_seed(P, lists[0], counts_at(0), counts_at(1), req_counts, c->stream); }));
+    if (spec) {   // the pixels' camera-ray triangle lists, once per render (timed with the seeding)
+        if ((rc = ensure(c, c->camlist, n * sizeof(uint4)))) return rc;
+        P.camlist = as<uint4>(c->camlist);
+        HIPCHK(c, launch(XRT_K_SEED, [&] { return launch_camlist(P, c->stream); }));
+    }
     if (pixel) {
         // every pixel of the shard in one persistent launch; the pixel counter is a stats word
         // (zeroed with them above)
@@ -963,7 +970,10 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     // a slot's ring is twisted at the end of a launch when fewer words are left than the next
     // launch can draw: the merged kernel draws at most step_merged_draws per segment and
     // checks it; k_step / k_step_tri check kRngVisit per visit
-    P.rng_keep = merged                      ? step_visits * step_merged_draws(P) + step_merged_draws(P)
+    // k_step_spec reads up to kSpecDraws words past the cursor per visit: fewer visits per launch
+    const uint32_t spec_visits = spec ? std::min<uint32_t>(step_visits, (kMT - kSpecDraws) / kSpecDraws) : 0;
+    P.rng_keep = spec ? std::max(step_visits * step_merged_draws(P) + step_merged_draws(P), spec_visits * kSpecDraws + kSpecDraws)
+                 : merged                      ? step_visits * step_merged_draws(P) + step_merged_draws(P)
                  : (volumetric && kVptEvents) ? step_visits * kVptEventDraws + kRngVisit
                                               : step_visits * kVisitDraws + kRngVisit;
     if (!pixel && P.rng_keep > kMT) return set_err(c, XRT_ERR_INVALID, "visits_per_launch too large for the RNG ring");
@@ -997,7 +1007,12 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
                 const uint32_t spw = step_merged_spw(P, live_hint);
                 S.layout_launches[spw == 64 ? 0 : spw == 32 ? 1 : spw == 16 ? 2 : spw == 8 ? 3 : 4]++;
             }
+            const bool spec_now = spec && step_merged_spw(P, live_hint) == 16 && step_merged_group(P, 16) == 4;
+            if (spec_now) S.spec_launches++;
             hipError_t e = launch(XRT_K_STEP, [&] {
+                if (spec_now)
+                    return launch_step_spec(P, dP, lists[cur], counts_at(ci), lists[nxt], counts_at(co), counts_at(cz),
+                                            spec_visits, live_part_max, c->stream);
                 if (merged)
                     return launch_step_merged(P, dP, c->step_objs, lists[cur], counts_at(ci), lists[nxt],
                                               counts_at(co), counts_at(cz), req_counts + (epoch & 1) * kMaxParts,
@@ -1252,6 +1267,7 @@ static int render_multi(xrt_ctx* m, const xrt_render_params* p, float* d_out, fl
             T.pix_windows += S[i].pix_windows, T.pix_stride4 += S[i].pix_stride4, T.pix_frustum += S[i].pix_frustum;
             T.pix_frustum_overflow += S[i].pix_frustum_overflow, T.pix_shadow_list += S[i].pix_shadow_list;
             T.pix_shadow_overflow += S[i].pix_shadow_overflow, T.pix_flushes += S[i].pix_flushes;
+            T.spec_launches += S[i].spec_launches;
             for (int k = 0; k < 5; ++k) T.layout_launches[k] += S[i].layout_launches[k];
             T.path_slots += S[i].path_slots;
             T.iterations = std::max(T.iterations, S[i].iterations);
