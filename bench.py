@@ -175,7 +175,7 @@ def main():
     ap.add_argument("--schedule", default="auto", choices=("auto", "step", "wavefront"))
     ap.add_argument("--traffic", default=None, help="default profiles/traffic_<CONFIG>.json")
     ap.add_argument("--pmc", default=None, help="default profiles/pmc_<CONFIG>.json")
-    ap.add_argument("--spec", action="store_true", help="speculative sample starts in 16-slot launches (XRT_FLAG_SPEC)")
+    ap.add_argument("--no-spec", action="store_true", help="no speculative sample starts (XRT_FLAG_NO_SPEC)")
     ap.add_argument("--assembly", default="gather", choices=("gather", "reduce"),
                     help="N > 1: frame assembly on rank 0 — gather each rank's owned rows, or reduce(SUM) full frames")
     ap.add_argument("--test-standin", default=None, metavar="MODULE:FACTORY",
@@ -254,7 +254,7 @@ def main():
         # reduce(SUM)); the render waits for the work queued on torch's stream (the previous
         # step's collective) before it overwrites fb
         return sharded.render(scene, W, H, fb, timing=timing and timed, schedule=args.schedule,
-                              **({"spec": True} if args.spec else {}))
+                              **({"spec": False} if args.no_spec else {}))
 
     for _ in range(args.warmup):
         step(False)

@@ -140,9 +140,10 @@ enum {
                                    depend on either                                            */
     XRT_FLAG_NO_PIXEL = 128u,   /* Direct / Normal: the per-slot fused schedule (k_step) instead
                                    of pixel-parallel sample chains (k_pixel); same results     */
-    XRT_FLAG_SPEC = 256u,       /* GI, one light, small triangle scenes: the merged schedule's
-                                   16-slot launches start every sample speculatively beside its
-                                   predecessor's last trace (k_step_spec); same results        */
+    XRT_FLAG_NO_SPEC = 256u,    /* GI, one light, small triangle scenes: the merged schedule's
+                                   16-slot launches start every sample beside its predecessor's
+                                   last trace (k_step_spec, the default); this flag keeps them on
+                                   k_step_merged — same results                                */
     XRT_FLAG_ACCUMULATE = 16u  /* Renderer::render's in-place contract (Src/renderer.cpp:75,98):
                                   each owned pixel starts from the value already in the output
                                   buffer (Image::addPixel adds to it in sample order), then

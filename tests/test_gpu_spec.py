@@ -6,7 +6,8 @@ the three stream offsets where the successor can start, and the lane whose offse
 confirms shades the successor's first hit in the same visit.  Bar: framebuffers bit for bit
 and every counter (Scene::intersect calls, shadow rays, draws, rejects) equal to the
 reference's sequential NormalRenderer::doRender (Src/renderer.cpp:29-81) as restated by the
-oracle.  Cases force the variant on every launch (slots_per_wave=16) and let the library mix
+oracle.  The variant is the default (XRT_FLAG_NO_SPEC turns it off: same image, no speculative
+launch).  Cases force it on every launch (slots_per_wave=16) and let the library mix
 it with the other layouts; cover launch boundaries (1-3 visits per launch: samples and
 pending shadow rays cross launches), depths 2-5, rejects with the in-place accumulate
 contract, the camera lists' covered / multi-triangle / empty pixels, and C2's own geometry
@@ -42,7 +43,7 @@ def renderer():
 def render_spec(r, scene, w, h, spp, force=True, **kw):
     r.spp = spp
     r._uploaded = None
-    img = r.render(scene, w, h, spec=True, timing=True, slots_per_wave=16 if force else 0, **kw)
+    img = r.render(scene, w, h, timing=True, slots_per_wave=16 if force else 0, **kw)
     g = r.stats
     okw = {k: v for k, v in kw.items() if k in ("integrator", "max_depth", "shard_index", "shard_count", "initial")}
     ref, st = pyoracle.render(scene, w, h, spp, **okw)
@@ -79,10 +80,11 @@ def test_depths(renderer, depth):
 
 
 def test_mixed_layouts_frame(renderer):
-    """The library's own layout choice: full waves while many slots live, the speculative
-    16-slot launches in the tail (and the 4-slot ones below that)."""
+    """The library's own layout choice for a 120k-pixel frame at 4 visits per launch: 32 slots
+    per wave while more than 90k slots live, then the speculative 16-slot launches (and the
+    4-slot layout below 20k) — slots move between the kernels mid-sample."""
     s = scenes.cornell(400, 300)
-    img, ref, st, g = render_spec(renderer, s, 400, 300, 24, force=False)
+    img, ref, st, g = render_spec(renderer, s, 400, 300, 24, force=False, visits_per_launch=4)
     compare(img, ref)
     ll = g.layout_launches
     assert g.spec_launches == ll[2] > 0 and ll[0] + ll[1] > 0
@@ -114,7 +116,7 @@ def test_c2_row_shard(renderer):
     renderer.spp = 64
     renderer.upload(scene)
     fb = torch.full((h, w, 3), 7.0, dtype=torch.float32, device="cuda:0")
-    renderer.render_device(scene, w, h, fb.data_ptr(), shard_index=3, shard_count=8, spec=True, slots_per_wave=16,
+    renderer.render_device(scene, w, h, fb.data_ptr(), shard_index=3, shard_count=8, slots_per_wave=16,
                            timing=True)
     g = renderer.stats
     assert g.spec_launches == g.launches[abi.XRT_K_STEP] > 0
@@ -125,3 +127,16 @@ def test_c2_row_shard(renderer):
     ref, st = pyoracle.render(scene, w, h, 64, shard_index=3, shard_count=8)
     compare(img[owned], ref[owned])
     assert (g.segments, g.shadow_rays, g.draws) == (st["segments"], st["shadow_rays"], st["draws"])
+
+
+def test_no_spec_flag_same_image(renderer):
+    """XRT_FLAG_NO_SPEC keeps the 16-slot launches on k_step_merged: the same image and counters."""
+    s = scenes.cornell(48, 36)
+    renderer.spp = 16
+    renderer._uploaded = None
+    a = renderer.render(s, 48, 36, slots_per_wave=16)
+    ga = renderer.stats
+    b = renderer.render(s, 48, 36, slots_per_wave=16, spec=False)
+    gb = renderer.stats
+    assert ga.spec_launches > 0 and gb.spec_launches == 0
+    assert np.array_equal(a, b) and (ga.segments, ga.draws) == (gb.segments, gb.draws)

@@ -1,14 +1,14 @@
 #!/bin/bash
-# tools/pmc_shard.sh TAG CONFIG N — one SQ instruction-mix pass over shard 0 of N row shards of
+# tools/pmc_shard.sh TAG CONFIG N [shard_sim args] — one SQ instruction-mix pass over shard 0 of N row shards of
 # CONFIG (tools/shard_sim.py --only=N: a warm-up render and the timed one), per kernel
 # instantiation: launches, VALU / SALU / LDS / VMEM / branch instructions per launch, wait and
 # VALU-active shares of the wave cycles
 set -uo pipefail
-TAG=$1; CFG=$2; N=$3
+TAG=$1; CFG=$2; N=$3; shift 3
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out/$TAG; mkdir -p "$O"; export TMPDIR=/tmp
 timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU \
-  -d "$O/ps" -o q --output-format csv -- python3 "$R/tools/shard_sim.py" "$CFG" --only="$N" > "$O/ps_${CFG}_$N.log" 2>&1 || exit $?
+  -d "$O/ps" -o q --output-format csv -- python3 "$R/tools/shard_sim.py" "$CFG" --only="$N" --reps=1 --warm-shard "$@" > "$O/ps_${CFG}_$N.log" 2>&1 || exit $?
 python3 - "$O/ps" > "$O/pmc_shard_${CFG}_$N.txt" <<'PY'
 import collections, csv, glob, sys
 acc = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -29,3 +29,4 @@ for k, c in sorted(acc.items(), key=lambda x: -x[1].get("SQ_INSTS_VALU", 0)):
 PY
 rm -rf "$O/ps"
 cat "$O/pmc_shard_${CFG}_$N.txt"
+

@@ -71,8 +71,11 @@ def main():
     r = HipRenderer(SPP, device=0)
     r.upload(scene)
     fb = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0")
-    kw = dict(slots_per_wave=spw, group=group, deep=deep, schedule=sched, spec="--spec" in sys.argv)
-    r.render_device(scene, W, H, fb.data_ptr(), shard_index=0, shard_count=1, **kw)   # warm: full-frame buffers
+    kw = dict(slots_per_wave=spw, group=group, deep=deep, schedule=sched, spec="--no-spec" not in sys.argv)
+    # warm: full-frame buffers (--warm-shard: the first measured shard instead, so a counter
+    # pass over the run sees that shard's launches only)
+    wn = (only[0] if only else 1) if "--warm-shard" in sys.argv else 1
+    r.render_device(scene, W, H, fb.data_ptr(), shard_index=0, shard_count=wn, **kw)
     torch.cuda.synchronize()
     res = {}
     for n in (only or (1, 2, 4, 8)):

@@ -27,7 +27,7 @@ XRT_INTEGRATOR_INDIRECT, XRT_INTEGRATOR_NORMAL, XRT_INTEGRATOR_VPT_NEE = 3, 4, 5
 XRT_MEDIUM_HETEROGENEOUS, XRT_MEDIUM_HOMOGENEOUS_MIS, XRT_MEDIUM_HOMOGENEOUS_ACHROMATIC, XRT_MEDIUM_HOMOGENEOUS_NOMIS = 0, 1, 2, 3
 XRT_FLAG_TIMING, XRT_FLAG_WAVEFRONT, XRT_FLAG_NO_MERGED, XRT_FLAG_NO_GROUP, XRT_FLAG_ACCUMULATE = 1, 2, 4, 8, 16
 XRT_FLAG_DEEP_SINGLE, XRT_FLAG_DEEP_QUAD, XRT_FLAG_NO_PIXEL = 32, 64, 128
-XRT_FLAG_SPEC = 256
+XRT_FLAG_NO_SPEC = 256
 XRT_SCHED_WAVEFRONT, XRT_SCHED_STEP, XRT_SCHED_STEP_TRI, XRT_SCHED_STEP_MERGED, XRT_SCHED_STEP_BVH = 0, 1, 2, 3, 4
 XRT_SCHED_PIXEL = 5
 SCHEDULE_NAMES = ("wavefront", "step", "step_tri", "step_merged", "step_bvh", "pixel")

@@ -176,7 +176,8 @@ __device__ __forceinline__ bool ray_tri_nb(v3 o, v3 d, v3 v0, v3 e1, v3 e2, floa
 // the group by DPP, lane u tests the candidate triangles k = u (mod G) in increasing k, and
 // the group reduces by DPP: min of (t bits << 32 | k) for the extension ray — smallest t,
 // then lowest index, the reference's in-order `t < best` scan — and OR of occlusion bits.
-template <int NL, int G>
+// LAZY: form each ray's o * inv per object test instead of keeping it (fewer live registers)
+template <int NL, int G, bool LAZY = false>
 __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const DObjPlane* pl, int lane, bool ext, v3 o, v3 d,
                                             uint32_t shm, const v3 (&so)[NL + 1], const v3 (&sd)[NL + 1],
                                             const float (&stm)[NL + 1], unsigned long long& best, uint32_t& occ) {
@@ -187,9 +188,12 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const D
 #pragma unroll
     for (int q = 0; q < R; ++q) tm[q] = 0ull;
     inv[0] = rcp3c(d);
-    oi[0] = o * inv[0];
+    if (!LAZY) oi[0] = o * inv[0];
 #pragma unroll
-    for (int l = 0; l < NL; ++l) inv[1 + l] = rcp3c(sd[l]), oi[1 + l] = so[l] * inv[1 + l];
+    for (int l = 0; l < NL; ++l) {
+        inv[1 + l] = rcp3c(sd[l]);
+        if (!LAZY) oi[1 + l] = so[l] * inv[1 + l];
+    }
     for (int ob0 = 0; ob0 < n_objs; ob0 += G) {
         const int ob = ob0 + u;
         if (ob < n_objs) {
@@ -197,11 +201,12 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const D
             const DObjPlane pb = pl[ob];
             const uint32_t cnt = (uint32_t)(B.count_occ & 0x7fffffff);
             const uint64_t bits = (cnt >= 64u ? ~0ull : ((1ull << cnt) - 1ull)) << B.first;
-            if (ext && !plane_away(o, d, pb.axis, pb.c) && box_overlap_f(oi[0], inv[0], B, kINF)) tm[0] |= bits;
+            if (ext && !plane_away(o, d, pb.axis, pb.c) && box_overlap_f(LAZY ? o * inv[0] : oi[0], inv[0], B, kINF))
+                tm[0] |= bits;
 #pragma unroll
             for (int l = 0; l < NL; ++l)
                 if (B.count_occ < 0 && ((shm >> l) & 1u) && !plane_away(so[l], sd[l], pb.axis, pb.c) &&
-                    box_overlap_f(oi[1 + l], inv[1 + l], B, stm[l]))
+                    box_overlap_f(LAZY ? so[l] * inv[1 + l] : oi[1 + l], inv[1 + l], B, stm[l]))
                     tm[1 + l] |= bits;
         }
     }

@@ -269,16 +269,18 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_spec(
         };
         // the quad's trace (every lane): lane 0's extension ray and shadow ray, lane 1's shadow
         // ray; then the shadow results and the finishes they complete, in sample order
+        // (broadcast in place: lanes 1-3 hold no extension ray, and the shadow rays are dead once
+        // traced — fewer registers live across the trace)
         auto trace_resolve = [&](bool ext_on, unsigned long long& best) {
             v3 so_t[3], sd_t[3];
             float stm_t[3];
-            so_t[0] = qb3<0>(so), sd_t[0] = qb3<0>(sd), stm_t[0] = qbf<0>(stm);
             so_t[1] = qb3<1>(so), sd_t[1] = qb3<1>(sd), stm_t[1] = qbf<1>(stm);
+            so_t[0] = so = qb3<0>(so), sd_t[0] = sd = qb3<0>(sd), stm_t[0] = stm = qbf<0>(stm);
             so_t[2] = sd_t[2] = mk(0, 0, 0), stm_t[2] = 0.0f;
             const uint32_t sh_t = (qb<0>(shm) & 1u) | ((qb<1>(shm) & 1u) << 1);
-            const v3 o_t = qb3<0>(o), d_t = qb3<0>(d);
+            o = qb3<0>(o), d = qb3<0>(d);
             uint32_t occ = 0;
-            group_trace<2, G>(P.n_objs, L, lplane, lane, ext_on, o_t, d_t, sh_t, so_t, sd_t, stm_t, best, occ);
+            group_trace<2, G>(P.n_objs, L, lplane, lane, ext_on, o, d, sh_t, so_t, sd_t, stm_t, best, occ);
             // GIIntegrator: rad += thr * directL (folded into c1 / c0z when it was sampled)
             if (u <= 1 && shm) {
                 rad = rad + (((occ >> u) & 1u) ? mk(zdecode(c0z & 3u), zdecode((c0z >> 2) & 3u), zdecode(c0z >> 4)) : c1);

@@ -844,7 +844,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     const bool fused = bvh || (!(p->flags & XRT_FLAG_WAVEFRONT) && step_lds_bytes(P) != 0);
     const bool merged = bvh || (fused && !(p->flags & XRT_FLAG_NO_MERGED) && use_step_merged(P));
     // speculative sample starts for the merged schedule's 16-slot launches (spec.hip)
-    const bool spec = merged && !bvh && (p->flags & XRT_FLAG_SPEC) && use_step_spec(P);
+    const bool spec = merged && !bvh && !(p->flags & XRT_FLAG_NO_SPEC) && use_step_spec(P);
     // live-list partitions (a multiple of the 8 XCDs): every wave appends to its partition's
     // counters once per launch, so more partitions mean less atomic contention (64 -> 256:
     // C4 -14%, C2 -4.5%).  The merged schedule (64 segments per launch) is fastest with

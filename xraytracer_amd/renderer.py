@@ -68,7 +68,7 @@ class HipRenderer:
 
     def params(self, scene, width, height, shard_index=0, shard_count=1, timing=False, integrator=None,
                max_depth=None, schedule="auto", slots_per_wave=0, visits_per_launch=0, group=True,
-               accumulate=False, deep="auto", spec=False):
+               accumulate=False, deep="auto", spec=True):
         """schedule: "auto" (fused k_step when the scene fits in LDS — for small triangle
         scenes with merged shadow + extension traces, for Direct / Normal pixel-parallel
         sample chains (k_pixel) — else the multi-pass wavefront), "step" (the per-slot fused
@@ -80,7 +80,8 @@ class HipRenderer:
         current contents before the divide (XRT_FLAG_ACCUMULATE, Renderer::render's contract).
         deep: the two-level trace's BVH walk, "auto", "single" (one lane per queued ray) or
         "quad" (four); results never depend on it.  spec: speculative sample starts in the merged
-        schedule's 16-slot launches (XRT_FLAG_SPEC, GI with one light); results never depend on it."""
+        schedule's 16-slot launches (GI with one light; spec=False sets XRT_FLAG_NO_SPEC); results
+        never depend on it."""
         if schedule not in ("auto", "step", "wavefront", "step_tri"):
             raise ValueError(f"unknown schedule {schedule!r}")
         if deep not in ("auto", "single", "quad"):
@@ -93,7 +94,7 @@ class HipRenderer:
         p.flags = ((abi.XRT_FLAG_TIMING if timing else 0) | (abi.XRT_FLAG_WAVEFRONT if schedule == "wavefront" else 0) |
                    (abi.XRT_FLAG_NO_MERGED if schedule == "step_tri" else 0) | (0 if group else abi.XRT_FLAG_NO_GROUP) |
                    (abi.XRT_FLAG_NO_PIXEL if schedule in ("step", "step_tri") else 0) |
-                   (abi.XRT_FLAG_ACCUMULATE if accumulate else 0) | (abi.XRT_FLAG_SPEC if spec else 0) |
+                   (abi.XRT_FLAG_ACCUMULATE if accumulate else 0) | (0 if spec else abi.XRT_FLAG_NO_SPEC) |
                    {"auto": 0, "single": abi.XRT_FLAG_DEEP_SINGLE, "quad": abi.XRT_FLAG_DEEP_QUAD}[deep])
         p.slots_per_wave, p.visits_per_launch = slots_per_wave, visits_per_launch
         return p
