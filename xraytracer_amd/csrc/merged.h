@@ -259,6 +259,25 @@ __device__ __forceinline__ void group_trace(int n_objs, const LScene& L, const D
     occ = group_or32<G>(oc);
 }
 
+// Scene::intersect for a camera ray of the pixel whose camera list (k_camlist, spec.hip) is
+// cl = {mask bits 0-31, 32-63, covering triangle or -1, 0}: the (t bits << 32 | triangle)
+// minimum over the listed triangles — every triangle a camera ray of the pixel can hit, less
+// those hidden behind a covering one — or, when one triangle covers the pixel alone, that
+// triangle (every camera ray of the pixel hits it first; the caller recomputes t, u, v).
+__device__ __forceinline__ unsigned long long camlist_closest(const LScene& L, uint4 cl, v3 o, v3 d) {
+    if ((int)cl.z >= 0) return (unsigned long long)cl.z;
+    unsigned long long best = ~0ull;
+    for (uint64_t bits = (uint64_t)cl.x | ((uint64_t)cl.y << 32); bits; bits &= bits - 1ull) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(bits);
+        float t;
+        if (ray_tri_nb(o, d, xyz(L.tri[3 * k]), xyz(L.tri[3 * k + 1]), xyz(L.tri[3 * k + 2]), t)) {
+            const unsigned long long key = ((unsigned long long)__float_as_uint(t) << 32) | k;
+            best = key < best ? key : best;
+        }
+    }
+    return best;
+}
+
 // LDS of k_step_merged: the scene (step_layout), the per-object planes (group traces), then
 // one MergedWave of trace scratch per wave
 __host__ __device__ inline uint32_t merged_plane_off(const StepLayout& Lo) { return (Lo.total + 15u) & ~15u; }

@@ -315,19 +315,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_spec(
                 const float uu = div_w(P, (float)(int)col + jx);
                 const float vv = div_h(P, (float)(int)row + jy);
                 camera_ray(P, uu, vv, o, d);
-                best = ~0ull;
-                if (cov >= 0) {
-                    best = (uint32_t)cov;   // every camera ray of the pixel hits it first (k_camlist)
-                } else {
-                    for (uint64_t bits = cm; bits; bits &= bits - 1ull) {
-                        const uint32_t kk = (uint32_t)__builtin_ctzll(bits);
-                        float t;
-                        if (ray_tri_nb(o, d, xyz(L.tri[3 * kk]), xyz(L.tri[3 * kk + 1]), xyz(L.tri[3 * kk + 2]), t)) {
-                            const unsigned long long key = ((unsigned long long)__float_as_uint(t) << 32) | kk;
-                            best = key < best ? key : best;
-                        }
-                    }
-                }
+                best = camlist_closest(L, make_uint4((uint32_t)cm, (uint32_t)(cm >> 32), (uint32_t)cov, 0u), o, d);
             }
             // ---- does the sample in progress end with this trace, and after how many words? (lane 0)
             bool endA = false;

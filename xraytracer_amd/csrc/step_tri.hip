@@ -622,16 +622,23 @@ __global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void 
             const bool act = live && !(st & ST_DONE) && g - rng.c >= (uint32_t)NW;
             if (!__ballot(act || shm)) break;
             const bool ext_now = act && ext;
+            // a sample's camera ray (depth 0) is tested against its pixel's camera list
+            // (k_camlist, spec.hip: the triangles a camera ray of the pixel can hit, or the one
+            // every such ray hits first) instead of taking part in the trace
+            const bool cam = XRT_MERGED_CAMLIST && !BVH && P.camlist && ext_now && depth == 0;
+            uint4 cl = make_uint4(0u, 0u, 0xffffffffu, 0u);
+            if (cam) cl = P.camlist[s];   // used after the trace: its latency hides behind it
             unsigned long long best;
             uint32_t occ;
             if constexpr (BVH) {
                 merged_trace<NL, true>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
                 deep_pass<NL, uint16_t>(P, top, ntop, stk, W, lane, root, ext_now, o, d, shm, so, sd, stm, best, occ);
             } else if constexpr (!LANE) {
-                merged_trace<NL>(SO, L, W, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
+                merged_trace<NL>(SO, L, W, lane, ext_now && !cam, o, d, shm, so, sd, stm, best, occ);
             } else {
-                group_trace<NL, G>(P.n_objs, L, lplane, lane, ext_now, o, d, shm, so, sd, stm, best, occ);
+                group_trace<NL, G>(P.n_objs, L, lplane, lane, ext_now && !cam, o, d, shm, so, sd, stm, best, occ);
             }
+            if (cam) best = camlist_closest(L, cl, o, d);
             resolve(occ);
             if (BVH ? pf_pending : vis > 0) rng.take();   // the words prefetched at the end of the previous segment
             if (ext_now) {

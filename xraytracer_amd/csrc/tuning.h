@@ -19,6 +19,10 @@
 #ifndef XRT_LIVE16
 #define XRT_LIVE16 20000     // below: 4 slots per wave (16 lanes each; group traces only)
 #endif
+#ifndef XRT_MERGED_CAMLIST
+#define XRT_MERGED_CAMLIST 0 // k_step_merged: camera rays from the pixel's camera list, not the trace (C2 1 GPU
+                             // 71.1 -> 71.7 ms, 8 shards 23.8 -> 23.9: -1.6% VALU, +8 spilled VGPRs); k_step_spec always
+#endif
 #ifndef XRT_TRACE_TLIM
 #define XRT_TRACE_TLIM 1     // merged_trace: cull objects beyond the ray's closest hit so far / after occlusion (C2 -1.2%)
 #endif

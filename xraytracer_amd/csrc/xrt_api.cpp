@@ -911,7 +911,11 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
         HIPCHK(c, hipMemcpyAsync(fb, h_out, npix * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(P.stats, 0, 512, c->stream));
     HIPCHK(c, launch(XRT_K_SEED, [&] { return launch_seed(P, lists[0], counts_at(0), counts_at(1), req_counts, c->stream); }));
-    if (spec) {   // the pixels' camera-ray triangle lists, once per render (timed with the seeding)
+    // the pixels' camera-ray triangle lists (small triangle scenes on the merged schedule: the
+    // camera rays' closest hits, and k_step_spec's candidates), once per render, timed with the
+    // seeding
+    P.camlist = nullptr;
+    if (merged && !bvh && P.n_tris <= 64 && !exp_env("XRT_NO_CAMLIST")) {
         if ((rc = ensure(c, c->camlist, n * sizeof(uint4)))) return rc;
         P.camlist = as<uint4>(c->camlist);
         HIPCHK(c, launch(XRT_K_SEED, [&] { return launch_camlist(P, c->stream); }));
@@ -1007,7 +1011,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
                 const uint32_t spw = step_merged_spw(P, live_hint);
                 S.layout_launches[spw == 64 ? 0 : spw == 32 ? 1 : spw == 16 ? 2 : spw == 8 ? 3 : 4]++;
             }
-            const bool spec_now = spec && step_merged_spw(P, live_hint) == 16 && step_merged_group(P, 16) == 4;
+            const bool spec_now = spec && P.camlist && step_merged_spw(P, live_hint) == 16 && step_merged_group(P, 16) == 4;
             if (spec_now) S.spec_launches++;
             hipError_t e = launch(XRT_K_STEP, [&] {
                 if (spec_now)
