@@ -203,6 +203,18 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_spec(
     lds_copy(const_cast<DObjPlane*>(lplane), P.obj_plane, P.n_objs, tid);
     __syncthreads();
     zero_parts(P, zero_count);
+    // experiment builds (XRT_PHASE_CLOCK, tools/phase.sh): shader-clock cycles per phase of a
+    // visit, per wave: loop head, trace, candidates, end test, shading, moves, cursor + reload,
+    // launch prologue / epilogue
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long t_ph = XRT_PHASE_CLOCK ? clock64() : 0ull;
+    auto tick = [&](int q) {
+        if constexpr (XRT_PHASE_CLOCK) {
+            const unsigned long long t = clock64();
+            ph[q] += t - t_ph;
+            t_ph = t;
+        }
+    };
     const int u = lane & 3;                                   // the lane's role in its quad
     const int qbase = lane & ~3;
     const uint32_t off = u == 2 ? 1u : (u == 3 ? 5u : 0u);    // its window / candidate offset
@@ -297,13 +309,16 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_spec(
             if (k >= spp) st = ST_DONE;
         };
         __builtin_amdgcn_s_waitcnt(0);   // prologue loads done: the loop waits only on its own prefetches
+        tick(7);
         for (uint32_t vis = 0; vis < visits; ++vis) {
             const bool act = live && !(st & ST_DONE) && g - cc >= kSpan;   // quad-uniform
             if (!__ballot(act || shm || fin)) break;
+            tick(0);
             const bool has0 = qb<0>(has ? 1u : 0u) != 0u;
             const uint32_t depth0 = qb<0>(depth);
             unsigned long long best = ~0ull;
             trace_resolve(act && has0, best);
+            tick(1);
             // ---- the candidates: the camera ray a successor starting at cursor + off traces
             // (Src/renderer.cpp:44-53), where a successor can start after this trace
             const bool more = kst < spp;
@@ -317,6 +332,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_spec(
                 camera_ray(P, uu, vv, o, d);
                 best = camlist_closest(L, make_uint4((uint32_t)cm, (uint32_t)(cm >> 32), (uint32_t)cov, 0u), o, d);
             }
+            tick(2);
             // ---- does the sample in progress end with this trace, and after how many words? (lane 0)
             bool endA = false;
             uint32_t xoff = 0;
@@ -343,6 +359,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_spec(
             const int bl = xoff == 0 ? 1 : (xoff == 1 ? 2 : 3);
             const bool isB = Bv && u == bl;
             const bool shadeA = u == 0 && act && has;
+            tick(3);
             if (isB) {   // a fresh path from the candidate's camera ray (o, d) and closest hit (best)
                 thr = mk(1, 1, 1), rad = mk(0, 0, 0), depth = 0;
                 shm = 0;
@@ -420,6 +437,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_spec(
                     if (depth >= max_depth) ended = true;
                 }
             }
+            tick(4);
             // ---- the quad's new state
             const uint32_t usedA = qb<0>(rng.c - c_in);          // words lane 0 drew in the shading
             const uint32_t usedB = qsel(rng.c - cc - off, qbase + bl);   // lane bl: jitter + its shading
@@ -460,12 +478,14 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_spec(
                 if (u == 3 || u == 2 || (u == 1 && !pendA)) shm = 0;
                 ++kst;
             }
+            tick(5);
             // the quad's cursor and the next windows
             if (act) cc = endA ? (Bv ? cc + xoff + usedB : cc + xoff) : cc + usedA;
             k = qb<0>(k);   // every finished sample is counted (pending ones are not yet)
             if (k >= spp) st = ST_DONE;
             rng.c = cc + off;
             rng.reload(ring);   // first read after the next visit's trace
+            tick(6);
         }
         // drain: the shadow rays still in flight and the samples waiting behind them, so no NEE
         // state crosses launches
@@ -497,6 +517,11 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_spec(
         }
         wave_append(live && lead && !(st & ST_DONE), s, out + it.p * P.part_cap, out_count + it.p, lane);
         wave_refill(P, want_req, s, g, lane, scratch);
+        tick(7);
+    }
+    if constexpr (XRT_PHASE_CLOCK) {
+        if (lane == 0)
+            for (int q = 0; q < 8; ++q) atomicAdd(P.stats + kStatsPhase + q, ph[q]);
     }
 }
 

@@ -105,6 +105,11 @@
 #define XRT_2A_WAVES 1       // k_trace_2a_coop launch bounds
 #endif
 
+// ---- experiment builds
+#ifndef XRT_PHASE_CLOCK
+#define XRT_PHASE_CLOCK 0    // k_step_spec: per-phase shader-clock cycles per wave into stats words 40..47
+#endif
+
 // ---- volumetric k_step (C5)
 #ifndef XRT_VPT_EVENTS
 #define XRT_VPT_EVENTS 1     // one event (a trace or one collision) per loop iteration

@@ -133,6 +133,7 @@ constexpr int kLargeObjTris = 256;  // two-level trace: mesh objects above this 
 constexpr int kSmallObjs = 256;
 constexpr unsigned kStepLds = 64u * 1024u;   // LDS budget of the fused schedule (k_step)
 constexpr int kStatsPix = 8;                // KParams::stats words 8..14: k_pixel path counters (xrt_stats pix_*)
+constexpr int kStatsPhase = 40;              // KParams::stats words 40..47: XRT_PHASE_CLOCK builds' phase cycles
 constexpr int kStatsWork = 32;               // KParams::stats word k_pixel counts the pixels taken in
 constexpr unsigned kPixLds = 160u * 1024u;   // k_pixel: scene + per-wave stream windows (gfx950: 160 KiB per workgroup)
 

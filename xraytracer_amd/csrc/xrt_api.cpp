@@ -911,15 +911,21 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
         HIPCHK(c, hipMemcpyAsync(fb, h_out, npix * 3 * sizeof(float), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(P.stats, 0, 512, c->stream));
     HIPCHK(c, launch(XRT_K_SEED, [&] { return launch_seed(P, lists[0], counts_at(0), counts_at(1), req_counts, c->stream); }));
-    // the pixels' camera-ray triangle lists (small triangle scenes on the merged schedule: the
-    // camera rays' closest hits, and k_step_spec's candidates), once per render, timed with the
-    // seeding
+    // the pixels' camera-ray triangle lists (small triangle scenes on the merged schedule:
+    // k_step_spec's candidates, and with XRT_MERGED_CAMLIST the merged kernel's camera rays),
+    // once per render, timed with the seeding; built before the first launch that reads them
     P.camlist = nullptr;
+    bool camlist_pending = false;
     if (merged && !bvh && P.n_tris <= 64 && !exp_env("XRT_NO_CAMLIST")) {
         if ((rc = ensure(c, c->camlist, n * sizeof(uint4)))) return rc;
         P.camlist = as<uint4>(c->camlist);
-        HIPCHK(c, launch(XRT_K_SEED, [&] { return launch_camlist(P, c->stream); }));
+        camlist_pending = true;
     }
+    auto build_camlist = [&]() -> hipError_t {
+        camlist_pending = false;
+        return launch(XRT_K_SEED, [&] { return launch_camlist(P, c->stream); });
+    };
+    if (camlist_pending && XRT_MERGED_CAMLIST) HIPCHK(c, build_camlist());
     if (pixel) {
         // every pixel of the shard in one persistent launch; the pixel counter is a stats word
         // (zeroed with them above)
@@ -1013,6 +1019,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
             }
             const bool spec_now = spec && P.camlist && step_merged_spw(P, live_hint) == 16 && step_merged_group(P, 16) == 4;
             if (spec_now) S.spec_launches++;
+            if (spec_now && camlist_pending) HIPCHK(c, build_camlist());
             hipError_t e = launch(XRT_K_STEP, [&] {
                 if (spec_now)
                     return launch_step_spec(P, dP, lists[cur], counts_at(ci), lists[nxt], counts_at(co), counts_at(cz),
@@ -1079,8 +1086,12 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
         for (uint32_t k = 0; k < P.n_part; ++k)
             if (left[k] != 0) return set_err(c, XRT_ERR_HIP, "iteration cap reached with live paths");
     }
-    unsigned long long hs[40] = {0};
-    HIPCHK(c, hipMemcpy(hs, P.stats, 40 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long hs[48] = {0};
+    HIPCHK(c, hipMemcpy(hs, P.stats, 48 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (XRT_PHASE_CLOCK)   // experiment builds: k_step_spec's visit phases (shader-clock cycles summed over waves)
+        std::fprintf(stderr, "[xrt] spec phase cycles head %llu trace %llu candidates %llu end-test %llu shading %llu"
+                     " moves %llu cursor+reload %llu launch %llu\n", hs[40], hs[41], hs[42], hs[43], hs[44], hs[45],
+                     hs[46], hs[47]);
     if (hs[38])   // experiment builds (-DXRT_EXPERIMENTS): BVH walk counters
         std::fprintf(stderr, "[xrt] deep rays %llu node steps %llu wave iterations %llu max wave iterations %llu"
                      " in-wave walks %llu\n", hs[38], hs[39], hs[37], hs[36], hs[35]);
