@@ -1,13 +1,14 @@
 """Speculative sample starts (k_step_spec, xraytracer_amd/csrc/spec.hip) against the oracle.
 
-In the merged schedule's 16-slot launches every GIIntegrator sample (Src/integrator.h:205-287)
+In the merged schedule's group layouts (16 slots of 4 lanes; the 4-slot tail, 16 lanes; 8
+slots of 8 lanes when forced) every GIIntegrator sample (Src/integrator.h:205-287)
 is started beside its predecessor's last trace: the slot's other lanes trace the camera rays of
 the three stream offsets where the successor can start, and the lane whose offset the trace
 confirms shades the successor's first hit in the same visit.  Bar: framebuffers bit for bit
 and every counter (Scene::intersect calls, shadow rays, draws, rejects) equal to the
 reference's sequential NormalRenderer::doRender (Src/renderer.cpp:29-81) as restated by the
 oracle.  The variant is the default (XRT_FLAG_NO_SPEC turns it off: same image, no speculative
-launch).  Cases force it on every launch (slots_per_wave=16) and let the library mix
+launch).  Cases force it on every launch (slots_per_wave=16, 8 or 4) and let the library mix
 it with the other layouts; cover launch boundaries (1-3 visits per launch: samples and
 pending shadow rays cross launches), depths 2-5, rejects with the in-place accumulate
 contract, the camera lists' covered / multi-triangle / empty pixels, and C2's own geometry
@@ -40,10 +41,10 @@ def renderer():
     r.close()
 
 
-def render_spec(r, scene, w, h, spp, force=True, **kw):
+def render_spec(r, scene, w, h, spp, force=True, spw=16, **kw):
     r.spp = spp
     r._uploaded = None
-    img = r.render(scene, w, h, timing=True, slots_per_wave=16 if force else 0, **kw)
+    img = r.render(scene, w, h, timing=True, slots_per_wave=spw if force else 0, **kw)
     g = r.stats
     okw = {k: v for k, v in kw.items() if k in ("integrator", "max_depth", "shard_index", "shard_count", "initial")}
     ref, st = pyoracle.render(scene, w, h, spp, **okw)
@@ -59,6 +60,16 @@ def test_cornell_every_launch_speculative(renderer, spp):
     img, ref, st, g = render_spec(renderer, s, 64, 48, spp)
     compare(img, ref)
     assert g.spec_launches == g.launches[abi.XRT_K_STEP] > 0
+
+
+@pytest.mark.parametrize("spw", [8, 4])
+def test_wider_groups(renderer, spw):
+    """8 and 16 lanes per slot (k_step_spec<8, 8>, <4, 16>: the quad and replicas of it that
+    widen the group trace), across launch boundaries."""
+    s = scenes.cornell(40, 30)
+    img, ref, st, g = render_spec(renderer, s, 40, 30, 11, spw=spw, visits_per_launch=3)
+    compare(img, ref)
+    assert g.spec_launches == g.launches[abi.XRT_K_STEP] > 5
 
 
 @pytest.mark.parametrize("visits", [1, 2, 3, 7])
@@ -81,13 +92,13 @@ def test_depths(renderer, depth):
 
 def test_mixed_layouts_frame(renderer):
     """The library's own layout choice for a 120k-pixel frame at 4 visits per launch: 32 slots
-    per wave while more than 90k slots live, then the speculative 16-slot launches (and the
-    4-slot layout below 20k) — slots move between the kernels mid-sample."""
+    per wave while more than 90k slots live, then the speculative 16-slot launches and, below
+    20k, the speculative 4-slot ones — slots move between the kernels mid-sample."""
     s = scenes.cornell(400, 300)
     img, ref, st, g = render_spec(renderer, s, 400, 300, 24, force=False, visits_per_launch=4)
     compare(img, ref)
     ll = g.layout_launches
-    assert g.spec_launches == ll[2] > 0 and ll[0] + ll[1] > 0
+    assert g.spec_launches == ll[2] + ll[4] and ll[2] > 0 and ll[4] > 0 and ll[0] + ll[1] > 0
 
 
 def test_rejects_and_accumulate(renderer):

@@ -61,15 +61,16 @@ hipError_t launch_step_merged(const KParams& P, const KParams* dP, const StepObj
                               const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
                               uint32_t* req_count, uint32_t visits, uint64_t live, uint32_t live_part_max,
                               hipStream_t st);
-// speculative sample starts for the merged schedule's 16-slot launches (spec.hip): eligibility,
-// the per-slot camera lists (once per render, after k_seed), and the step launch (same list /
-// counter contract as launch_step_merged)
+// speculative sample starts for the merged schedule's group layouts (spec.hip): eligibility,
+// the per-slot camera lists (once per render, before the first speculative launch), and the
+// step launch at spw = 16, 8 or 4 slots per wave (same list / counter contract as
+// launch_step_merged)
 bool use_step_spec(const KParams& P);
 constexpr uint32_t kSpecDraws = 11;   // stream words one k_step_spec visit may read past the cursor
 hipError_t launch_camlist(const KParams& P, hipStream_t st);
 hipError_t launch_step_spec(const KParams& P, const KParams* dP, const uint32_t* list, const uint32_t* count,
                             uint32_t* out, uint32_t* out_count, uint32_t* zero, uint32_t visits, uint32_t part_live,
-                            hipStream_t st);
+                            uint32_t spw, hipStream_t st);
 // the merged schedule's refill (leaves ST_RNGREQ to the merged kernel; see step_tri.hip)
 hipError_t launch_refill_merged(const KParams& P, const uint32_t* count, uint32_t* zero_count, hipStream_t st);
 hipError_t launch_finish(const KParams& P, hipStream_t st);

@@ -175,7 +175,9 @@ template <int SPW, int G>
 __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_spec(
     const KParams* __restrict__ Pp, const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
     uint32_t* __restrict__ out, uint32_t* out_count, uint32_t* zero_count, uint32_t visits) {
-    static_assert(G == 4 && SPW * G == 64, "one slot per quad of lanes");
+    // G lanes per slot: the slot's quad (roles below) and, for G = 8 or 16, replicas of it that
+    // run the same code on the same state and only widen the slot's group trace
+    static_assert((G == 4 || G == 8 || G == 16) && SPW * G == 64, "a slot per group of 4, 8 or 16 lanes");
     constexpr int NL = 1;            // one area light (use_step_spec)
     constexpr int NW = 6;            // stream words per lane window
     constexpr uint32_t kSpan = kSpecDraws;   // the quad's windows reach cursor + 10
@@ -223,7 +225,7 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_spec(
     for (uint32_t base = it.first; base < it.n; base += it.stride) {
         const uint32_t i = base + (uint32_t)(tid >> 6) * SPW + (uint32_t)lane / G;
         const bool own = lane / G < SPW && i < it.n;
-        const bool lead = own && u == 0;
+        const bool lead = own && (lane & (G - 1)) == 0;   // writes the slot back
         const uint32_t s = own ? list[it.p * P.part_cap + i] : 0;
         uint32_t st = own ? glb<gu32>(P.state)[s] : ST_DONE;
         st &= ~ST_RNGREQ;
@@ -311,6 +313,22 @@ __global__ __launch_bounds__(kBlock, XRT_STEP_WAVES) void k_step_spec(
         __builtin_amdgcn_s_waitcnt(0);   // prologue loads done: the loop waits only on its own prefetches
         tick(7);
         for (uint32_t vis = 0; vis < visits; ++vis) {
+            if (XRT_SPEC_TWIST) {
+                // a slot whose windows would reach past its generated words twists its ring here,
+                // the wave together as at the launch end (the block it overwrites is consumed:
+                // fewer than kSpan words are left), so launches need not end for the RNG
+                const bool need = live && !(st & ST_DONE) && g - cc < kSpan;   // group-uniform
+                if (__ballot(need)) {
+                    wave_refill(P, need && lead, s, g, lane, scratch);
+                    // the new words are read back below by other lanes of this wave: stores
+                    // done and this CU's L1 invalidated first
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+                    if (need) {
+                        g += kMT;
+                        rng.reload(ring);
+                    }
+                }
+            }
             const bool act = live && !(st & ST_DONE) && g - cc >= kSpan;   // quad-uniform
             if (!__ballot(act || shm || fin)) break;
             tick(0);
@@ -540,11 +558,21 @@ hipError_t launch_camlist(const KParams& P, hipStream_t st) {
 
 hipError_t launch_step_spec(const KParams& P, const KParams* dP, const uint32_t* list, const uint32_t* count,
                             uint32_t* out, uint32_t* out_count, uint32_t* zero, uint32_t visits, uint32_t part_live,
-                            hipStream_t st) {
-    constexpr uint32_t per_block = (kBlock / 64) * 16;
+                            uint32_t spw, hipStream_t st) {
+    const uint32_t per_block = (kBlock / 64) * spw;
     const uint32_t blocks = P.n_part * ((std::min(part_live, P.part_cap) + per_block - 1) / per_block);
-    hipLaunchKernelGGL((k_step_spec<16, 4>), dim3(blocks), dim3(kBlock), step_merged_lds_bytes(P), st, dP, list, count,
-                       out, out_count, zero, visits);
+    const size_t lds = step_merged_lds_bytes(P);
+    if (spw == 16)
+        hipLaunchKernelGGL((k_step_spec<16, 4>), dim3(blocks), dim3(kBlock), lds, st, dP, list, count, out, out_count,
+                           zero, visits);
+    else if (spw == 8)
+        hipLaunchKernelGGL((k_step_spec<8, 8>), dim3(blocks), dim3(kBlock), lds, st, dP, list, count, out, out_count,
+                           zero, visits);
+    else if (spw == 4)
+        hipLaunchKernelGGL((k_step_spec<4, 16>), dim3(blocks), dim3(kBlock), lds, st, dP, list, count, out, out_count,
+                           zero, visits);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -939,7 +939,9 @@ uint32_t step_merged_spw(const KParams& P, uint64_t live) {
     // issue, sets the time)
     if (live >= kMergedLive64) return 64;
     if (live >= kMergedLive32) return 32;
-    return live >= kMergedLive16 || !group ? 16u : 4u;
+    if (!group) return 16u;
+    if (live < kMergedLive16) return 4u;
+    return live < XRT_LIVE8 ? 8u : 16u;
 }
 
 // lanes that share one slot's traces at `spw` slots per wave (1 = pair passes over the wave)

@@ -16,6 +16,9 @@
 #ifndef XRT_LIVE32
 #define XRT_LIVE32 90000     // below: 16 slots per wave (4 lanes each), above: 32
 #endif
+#ifndef XRT_LIVE8
+#define XRT_LIVE8 0          // below (and above XRT_LIVE16): 8 slots per wave (8 lanes each; group traces only)
+#endif
 #ifndef XRT_LIVE16
 #define XRT_LIVE16 20000     // below: 4 slots per wave (16 lanes each; group traces only)
 #endif
@@ -103,6 +106,16 @@
 #endif
 #ifndef XRT_2A_WAVES
 #define XRT_2A_WAVES 1       // k_trace_2a_coop launch bounds
+#endif
+
+#ifndef XRT_SPEC_TWIST
+#define XRT_SPEC_TWIST 1     // k_step_spec twists a slot's RNG ring in-loop when its words run short
+#endif
+#ifndef XRT_SPEC_VISITS
+#define XRT_SPEC_VISITS 80   // ... so its launches run this many visits (without: kMT / kSpecDraws = 55); 48, 64, 128, 256: slower
+#endif
+#ifndef XRT_SPEC_TAIL
+#define XRT_SPEC_TAIL 1      // speculative starts in the 4-slot tail launches too (k_step_spec<4, 16>)
 #endif
 
 // ---- experiment builds

@@ -981,8 +981,12 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
     // launch can draw: the merged kernel draws at most step_merged_draws per segment and
     // checks it; k_step / k_step_tri check kRngVisit per visit
     // k_step_spec reads up to kSpecDraws words past the cursor per visit: fewer visits per launch
-    const uint32_t spec_visits = spec ? std::min<uint32_t>(step_visits, (kMT - kSpecDraws) / kSpecDraws) : 0;
-    P.rng_keep = spec ? std::max(step_visits * step_merged_draws(P) + step_merged_draws(P), spec_visits * kSpecDraws + kSpecDraws)
+    // (with XRT_SPEC_TWIST it twists in-loop instead: XRT_SPEC_VISITS visits unless the caller sets them)
+    const uint32_t spec_visits = !spec ? 0
+                                 : XRT_SPEC_TWIST ? ((ev || p->visits_per_launch) ? step_visits : XRT_SPEC_VISITS)
+                                                  : std::min<uint32_t>(step_visits, (kMT - kSpecDraws) / kSpecDraws);
+    P.rng_keep = spec && !XRT_SPEC_TWIST
+                     ? std::max(step_visits * step_merged_draws(P) + step_merged_draws(P), spec_visits * kSpecDraws + kSpecDraws)
                  : merged                      ? step_visits * step_merged_draws(P) + step_merged_draws(P)
                  : (volumetric && kVptEvents) ? step_visits * kVptEventDraws + kRngVisit
                                               : step_visits * kVisitDraws + kRngVisit;
@@ -1017,13 +1021,16 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
                 const uint32_t spw = step_merged_spw(P, live_hint);
                 S.layout_launches[spw == 64 ? 0 : spw == 32 ? 1 : spw == 16 ? 2 : spw == 8 ? 3 : 4]++;
             }
-            const bool spec_now = spec && P.camlist && step_merged_spw(P, live_hint) == 16 && step_merged_group(P, 16) == 4;
+            // speculative starts in the group layouts (4 lanes per slot; 16 in the tail; 8 when forced)
+            const uint32_t spw_now = merged ? step_merged_spw(P, live_hint) : 0;
+            const bool spec_now = spec && P.camlist && (spw_now == 16 || spw_now == 8 || (XRT_SPEC_TAIL && spw_now == 4)) &&
+                                  step_merged_group(P, spw_now) * spw_now == 64;
             if (spec_now) S.spec_launches++;
             if (spec_now && camlist_pending) HIPCHK(c, build_camlist());
             hipError_t e = launch(XRT_K_STEP, [&] {
                 if (spec_now)
                     return launch_step_spec(P, dP, lists[cur], counts_at(ci), lists[nxt], counts_at(co), counts_at(cz),
-                                            spec_visits, live_part_max, c->stream);
+                                            spec_visits, live_part_max, spw_now, c->stream);
                 if (merged)
                     return launch_step_merged(P, dP, c->step_objs, lists[cur], counts_at(ci), lists[nxt],
                                               counts_at(co), counts_at(cz), req_counts + (epoch & 1) * kMaxParts,
