@@ -13,7 +13,9 @@ import csv, glob, sys
 rows = list(csv.DictReader(open(glob.glob(sys.argv[1] + "/*kernel_stats.csv")[0])))
 top = max(rows, key=lambda r: float(r["TotalDurationNs"]))
 import re
-print(re.search(r"(k_\w+)", top["Name"]).group(1))
+k = re.search(r"(k_\w+)", top["Name"]).group(1)
+# the merged schedule's step launches (xrt_stats' XRT_K_STEP family) include the speculative kernel
+print("k_step_merged|k_step_spec" if k == "k_step_merged" else k)
 PY
 )
 python3 "$R/tools/prof_summary.py" "$R/gpurun_out/$TAG" "$KPAT" --traffic "$CFG" "$R/profiles/traffic_$CFG.json" \

@@ -31,7 +31,10 @@ def main():
         csv_out = args[i + 1]
         del args[i:i + 2]
     d = args[0]
+    # a kernel family: a name or a regex of names (e.g. "k_step_merged|k_step_spec": the merged
+    # schedule's step launches, which xrt_stats times as one family), keyed by its first name
     pat = args[1] if len(args) > 1 else "k_step"
+    fam = re.compile(pat)
     st = glob.glob(os.path.join(d, "kt", "*kernel_stats.csv"))
     # the kernel family's average launch: every dispatch of every instantiation whose name
     # matches (e.g. k_step_merged's 64-, 32- and 16-slot layouts), total time / total calls
@@ -41,7 +44,7 @@ def main():
         for r in csv.DictReader(open(st[0])):
             print(f'{float(r["TotalDurationNs"]) / 1e6:9.3f} ms {int(r["Calls"]):6d} calls '
                   f'avg {float(r["AverageNs"]) / 1e3:9.2f} us  {r["Name"][:80]}')
-            if pat in r["Name"]:
+            if fam.search(r["Name"]):
                 fam_ns += float(r["TotalDurationNs"])
                 fam_calls += int(r["Calls"])
         if fam_calls:
@@ -52,13 +55,13 @@ def main():
     rows = []
     for f in sorted(glob.glob(os.path.join(d, "*", "*counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
-            if pat in r["Kernel_Name"]:
+            if fam.search(r["Kernel_Name"]):
                 acc[r["Counter_Name"]] += float(r["Counter_Value"])
                 n[r["Counter_Name"]] += 1
                 rows.append((os.path.basename(os.path.dirname(f)), r.get("Dispatch_Id", ""), r["Counter_Name"],
                              r["Counter_Value"]))
                 if kname is None:
-                    m = re.search(r"(k_\w+)", r["Kernel_Name"])
+                    m = re.search(r"(k_\w+)", pat if "|" in pat else r["Kernel_Name"])
                     kname = m.group(1) if m else pat
     for k in sorted(acc):
         print(f"{k:28s} {acc[k]:.4g}  ({n[k]} dispatches)")
