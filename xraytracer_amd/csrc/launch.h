@@ -46,7 +46,7 @@ hipError_t launch_pixel(const KParams& P, uint32_t* work, hipStream_t st);
 // dP: device copy of P (the triangle-scene kernel reads its parameters from memory)
 hipError_t launch_step(const KParams& P, const KParams* dP, const uint32_t* list, const uint32_t* count, uint32_t* out,
                        uint32_t* out_count, uint32_t* zero, uint32_t* req_count, uint32_t visits, uint32_t blocks,
-                       hipStream_t st);
+                       uint64_t live, hipStream_t st);
 // merged-trace triangle schedule (step_tri.hip): eligibility, RNG words one segment may
 // draw, LDS bytes, the per-object kernel-argument records, and the launch (same list /
 // counter contract as launch_step)

@@ -133,6 +133,9 @@
 #ifndef XRT_VPT_EV_DRAWS
 #define XRT_VPT_EV_DRAWS 4   // ... draws of an event for the refill threshold (a collision draws <= 5)
 #endif
+#ifndef XRT_VPT_LOW_LIVE
+#define XRT_VPT_LOW_LIVE 131072   // ... live slots below which k_step runs its 2-wave build (2 waves x 1,024 SIMDs x 64)
+#endif
 #ifndef XRT_VPT_EV_PF
 #define XRT_VPT_EV_PF 4      // ... reload the 8-word RNG window below this many words
 #endif

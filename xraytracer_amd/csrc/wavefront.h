@@ -46,7 +46,8 @@ constexpr bool kVptEvents = XRT_VPT_EVENTS != 0;   // VPT k_step: one event (tra
 constexpr uint32_t kVptEventVisits = XRT_VPT_EV_VISITS;   // ... events per slot per launch
 constexpr uint32_t kVptEventDraws = XRT_VPT_EV_DRAWS;     // ... draws of an event for the refill threshold (a
                                            // collision draws <= 5; a lane with fewer words left stops early)
-constexpr uint32_t kVptEventPrefetch = XRT_VPT_EV_PF;     // ... reload the 8-word RNG window below this many
+constexpr uint32_t kVptEventPrefetch = XRT_VPT_EV_PF;
+constexpr uint64_t kVptLowLive = XRT_VPT_LOW_LIVE;          // ... below this many live slots: the 2-wave k_step build     // ... reload the 8-word RNG window below this many
 constexpr bool kStepBlock512 = XRT_KSTEP_512 != 0;   // k_step of sphere-BVH scenes in 512-thread blocks
 constexpr uint32_t kVisitDraws = 13; // max RNG draws of one GI/Direct segment (4 lights)
 // fused schedule: a slot's ring is twisted at the end of a step launch when fewer than

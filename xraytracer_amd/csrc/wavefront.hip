@@ -1516,8 +1516,10 @@ __device__ int nee_resume(const KParams& P, uint32_t s, v3 thr_m, v3& rad, Rng& 
     return 0;
 }
 
-template <int SCN, int INTEG, int BS = kBlock>
-__global__ __launch_bounds__(BS, XRT_KSTEP_WAVES) void k_step(KParams P, const uint32_t* __restrict__ list,
+// WV: waves per SIMD the register budget is sized for (XRT_KSTEP_WAVES; the volumetric
+// integrators also at 2, for launches with too few live slots to fill more: no spills)
+template <int SCN, int INTEG, int BS = kBlock, int WV = XRT_KSTEP_WAVES>
+__global__ __launch_bounds__(BS, WV) void k_step(KParams P, const uint32_t* __restrict__ list,
                                                   const uint32_t* __restrict__ count, uint32_t* __restrict__ out,
                                                   uint32_t* out_count, uint32_t* zero_count, uint32_t* req_count,
                                                   uint32_t visits) {
@@ -2405,7 +2407,7 @@ static size_t kstep_lds_bytes(const KParams& P, int bs) {
 template <int SCN>
 static hipError_t step_i(const KParams& P, const uint32_t* list, const uint32_t* count, uint32_t* out,
                          uint32_t* out_count, uint32_t* zero, uint32_t* req_count, uint32_t visits, uint32_t blocks,
-                         hipStream_t st) {
+                         uint64_t live, hipStream_t st) {
     // Sphere-BVH scenes (C3) keep ~45 KB of BVH and spheres in LDS, so 256-thread blocks stop
     // at 3 per CU (3 waves per SIMD); 512-thread blocks share one copy between 8 waves
     // (4 waves per SIMD, the VGPR limit).  Same partitions, same results.
@@ -2421,6 +2423,15 @@ static hipError_t step_i(const KParams& P, const uint32_t* list, const uint32_t*
     if (P.integrator == XRT_INTEGRATOR_DIRECT)
         hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_DIRECT>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
                            out, out_count, zero, req_count, visits);
+    // volumetric walks with fewer live slots than 2 waves per SIMD hold (a row shard of a
+    // multi-GPU frame, a frame's tail): the 2-wave build, whose registers hold the walk without
+    // spilling (C5 shard 0 of 8: 43.9 -> 41.9 ms; a full frame stays at 4 waves per SIMD)
+    else if (P.integrator == XRT_INTEGRATOR_VPT && live < kVptLowLive)
+        hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_VPT, kBlock, 2>), dim3(blocks), dim3(kBlock), lds, st, P, list,
+                           count, out, out_count, zero, req_count, visits);
+    else if (P.integrator == XRT_INTEGRATOR_VPT_NEE && live < kVptLowLive)
+        hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_VPT_NEE, kBlock, 2>), dim3(blocks), dim3(kBlock), lds, st, P,
+                           list, count, out, out_count, zero, req_count, visits);
     else if (P.integrator == XRT_INTEGRATOR_VPT)
         hipLaunchKernelGGL((k_step<SCN, XRT_INTEGRATOR_VPT>), dim3(blocks), dim3(kBlock), lds, st, P, list, count,
                            out, out_count, zero, req_count, visits);
@@ -2447,7 +2458,7 @@ bool use_step_tri(const KParams& P) {
 
 hipError_t launch_step(const KParams& P, const KParams* dP, const uint32_t* list, const uint32_t* count, uint32_t* out,
                        uint32_t* out_count, uint32_t* zero, uint32_t* req_count, uint32_t visits, uint32_t blocks,
-                       hipStream_t st) {
+                       uint64_t live, hipStream_t st) {
     if (!step_lds_bytes(P)) return hipErrorInvalidValue;
     if (P.n_part == 0 || blocks % P.n_part != 0) return hipErrorInvalidValue;   // part_iter's grid contract
     if (use_step_tri(P)) {
@@ -2461,9 +2472,9 @@ hipError_t launch_step(const KParams& P, const KParams* dP, const uint32_t* list
         return hipGetLastError();
     }
     switch (P.scene_kind) {
-        case SCN_TRI: return step_i<SCN_TRI>(P, list, count, out, out_count, zero, req_count, visits, blocks, st);
-        case SCN_SPHERE: return step_i<SCN_SPHERE>(P, list, count, out, out_count, zero, req_count, visits, blocks, st);
-        default: return step_i<SCN_MIXED>(P, list, count, out, out_count, zero, req_count, visits, blocks, st);
+        case SCN_TRI: return step_i<SCN_TRI>(P, list, count, out, out_count, zero, req_count, visits, blocks, live, st);
+        case SCN_SPHERE: return step_i<SCN_SPHERE>(P, list, count, out, out_count, zero, req_count, visits, blocks, live, st);
+        default: return step_i<SCN_MIXED>(P, list, count, out, out_count, zero, req_count, visits, blocks, live, st);
     }
 }
 

@@ -1036,7 +1036,7 @@ static int render_impl(xrt_ctx* c, const xrt_render_params* p, float* d_out, flo
                                               counts_at(co), counts_at(cz), req_counts + (epoch & 1) * kMaxParts,
                                               step_visits, live_hint, live_part_max, c->stream);
                 return launch_step(P, dP, lists[cur], counts_at(ci), lists[nxt], counts_at(co), counts_at(cz),
-                                   req_counts + (epoch & 1) * kMaxParts, step_visits, blocks, c->stream);
+                                   req_counts + (epoch & 1) * kMaxParts, step_visits, blocks, live_hint, c->stream);
             });
             if (e != hipSuccess) return hip_err(c, e, "k_step");
             // both step kernels refill their slots' rings themselves (wave_refill)
