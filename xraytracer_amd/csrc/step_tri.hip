@@ -434,8 +434,10 @@ hipError_t launch_trace_2a_coop(const KParams& P, const uint32_t* list, const ui
 // the hit triangle's shading data from global memory.  Same path
 // code otherwise.
 
-template <int INTEG, int NL, int SPW, int G, bool LANE, bool BVH>
-__global__ __launch_bounds__(kBlock, BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES) void k_step_merged(
+// WV (two-level scenes): a register budget for WV waves per SIMD instead of XRT_BVH_WAVES, for
+// launches with too few live slots to fill more (fewer spills)
+template <int INTEG, int NL, int SPW, int G, bool LANE, bool BVH, int WV = 0>
+__global__ __launch_bounds__(kBlock, WV ? WV : (BVH ? XRT_BVH_WAVES : XRT_STEP_WAVES)) void k_step_merged(
     const KParams* __restrict__ Pp, const StepObjs SO, const uint32_t* __restrict__ list,
     const uint32_t* __restrict__ count, uint32_t* __restrict__ out, uint32_t* out_count, uint32_t* zero_count,
     uint32_t* req_count, uint32_t visits) {
@@ -896,7 +898,7 @@ void build_step_objs(const DObjBox* boxes, const DObjPlane* planes, int n, StepO
     }
 }
 
-template <int INTEG, int SPW, int G, bool LANE, bool BVH = false>
+template <int INTEG, int SPW, int G, bool LANE, bool BVH = false, int WV = 0>
 static void launch_merged_i(const KParams& P, const KParams* dP, const StepObjs& SO, const uint32_t* list,
                             const uint32_t* count, uint32_t* out, uint32_t* out_count, uint32_t* zero,
                             uint32_t* req_count, uint32_t visits, uint32_t part_live, size_t lds, hipStream_t st) {
@@ -905,7 +907,7 @@ static void launch_merged_i(const KParams& P, const KParams* dP, const StepObjs&
     const uint32_t per_block = (kBlock / 64) * SPW;
     const uint32_t blocks = P.n_part * ((std::min(part_live, P.part_cap) + per_block - 1) / per_block);
 #define XRT_LAUNCH_MERGED(NLV)                                                                                       \
-    hipLaunchKernelGGL((k_step_merged<INTEG, NLV, SPW, G, LANE, BVH>), dim3(blocks), dim3(kBlock), lds, st, dP, SO, list, \
+    hipLaunchKernelGGL((k_step_merged<INTEG, NLV, SPW, G, LANE, BVH, WV>), dim3(blocks), dim3(kBlock), lds, st, dP, SO, list, \
                        count, out, out_count, zero, req_count, visits)
     if constexpr (BVH) {   // use_step_bvh: 1 or 2 lights
         if (P.n_lights == 1) XRT_LAUNCH_MERGED(1);
@@ -964,7 +966,15 @@ static void launch_merged_spw(const KParams& P, const KParams* dP, const StepObj
         switch (step_merged_spw(P, live)) {
             case 64: XRT_BVH_CASE(64); break;
             case 32: XRT_BVH_CASE(32); break;
-            default: XRT_BVH_CASE(16); break;
+            default:
+                // below XRT_BVH_LOW_LIVE live slots (a frame's or a row shard's tail) the
+                // XRT_BVH_LOW_WAVES build: more registers per wave, fewer spills
+                if (live < XRT_BVH_LOW_LIVE)
+                    launch_merged_i<INTEG, 16, 1, false, true, XRT_BVH_LOW_WAVES>(
+                        P, dP, *P.sstep, list, count, out, out_count, zero, req_count, visits, part_live, lds, st);
+                else
+                    XRT_BVH_CASE(16);
+                break;
         }
 #undef XRT_BVH_CASE
         return;

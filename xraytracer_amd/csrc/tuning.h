@@ -87,6 +87,12 @@
 #ifndef XRT_BVH_LEAF
 #define XRT_BVH_LEAF 4       // triangles per leaf of the triangle BVH (at most)
 #endif
+#ifndef XRT_BVH_LOW_LIVE
+#define XRT_BVH_LOW_LIVE 0       // two-level merged kernel: below this many live slots, the XRT_BVH_LOW_WAVES build (0: never)
+#endif
+#ifndef XRT_BVH_LOW_WAVES
+#define XRT_BVH_LOW_WAVES 3
+#endif
 #ifndef XRT_BVH_TOP
 #define XRT_BVH_TOP 64       // top 4-wide BVH nodes kept in LDS (at most; kStepLds bounds it); 192: neutral
 #endif
